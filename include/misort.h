@@ -1,0 +1,151 @@
+/*
+ * misort.h -- C-ABI of the MI355X-native bitonic sort (libmisort.so).
+ *
+ * Drop-in boundary for the hot path of masrul/Parallel-Computing-MPI's
+ * Parallel-Sorting/src/psort.cc.  The reference has no FFI: its swappable unit
+ * is the C++ function
+ *
+ *     double* parallel_bitonic_sort(double* buffer, int& loc_buf_size,
+ *                                   int max_size);              // psort.cc:167
+ *
+ * driven by the globals numprocs/myid of MPI_COMM_WORLD (psort.cc:107,535-536),
+ * with compare_split_{max,min} (psort.cc:116-164) exchanging whole blocks over
+ * MPI_Sendrecv.  Here ranks are GPUs (one process per GPU), the communicator is
+ * RCCL over xGMI, and keys live in HBM.  All entry points are extern "C", take
+ * plain pointers and sizes, return 0 on success or a negative MISORT_E_* code
+ * (message via misort_last_error()), and never throw.  A context is not
+ * thread-safe; use one per thread/GPU.
+ *
+ * Device pointers are HIP device addresses on the context's GPU.  `stream` is a
+ * hipStream_t (NULL = the context's own stream); calls are asynchronous on it
+ * unless stated otherwise.
+ */
+#ifndef MISORT_H
+#define MISORT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MISORT_VERSION 1
+
+/* Key types.  F64 keys are IEEE doubles compared as doubles (psort.cc sorts
+ * double); they are sorted as order-preserving 64-bit patterns, so results are
+ * bit-exact with the reference except for mixtures of -0.0/+0.0 or NaNs, whose
+ * relative order std::sort leaves unspecified. */
+enum misort_dtype { MISORT_U32 = 0, MISORT_U64 = 1, MISORT_F64 = 2 };
+
+enum misort_status {
+    MISORT_OK = 0,
+    MISORT_E_INVALID = -1,   /* bad argument */
+    MISORT_E_NOT_POW2 = -2,  /* psort.cc:168-172 "bitonic sort requires 2^d processors" */
+    MISORT_E_HIP = -3,       /* HIP runtime error */
+    MISORT_E_RCCL = -4,      /* RCCL error */
+    MISORT_E_NO_COMM = -5,   /* communicator not initialised */
+    MISORT_E_CAPACITY = -6   /* a partner block exceeds max_size (MPI_Sendrecv truncation) */
+};
+
+/* Kernel families reported by the per-launch profiler. */
+enum misort_kernel_kind {
+    MISORT_K_TILE_SORT = 0,   /* levels 1..LT in one LDS tile            */
+    MISORT_K_GLOBAL = 1,      /* fused large-stride HBM pass             */
+    MISORT_K_TILE_MERGE = 2,  /* in-tile strides of one merge level      */
+    MISORT_K_MERGE_SPLIT = 3, /* device compare-split (psort.cc:116-164) */
+    MISORT_K_OTHER = 4
+};
+
+typedef struct misort_ctx misort_ctx;
+
+int misort_version(void);
+const char* misort_last_error(void);
+
+/* Context on HIP device `device`: selects it, creates a non-blocking stream and
+ * grows scratch buffers on demand.  Replaces MPI_Init's per-process setup. */
+int misort_create(int device, misort_ctx** out);
+int misort_destroy(misort_ctx* ctx);
+/* hipStream_t of the context (as void*). */
+void* misort_stream(misort_ctx* ctx);
+int misort_synchronize(misort_ctx* ctx);
+
+/* ---- communicator (replaces MPI_COMM_WORLD, psort.cc:107,535-536) -------- */
+#define MISORT_UNIQUE_ID_BYTES 128
+/* Rank 0 creates the id (ncclGetUniqueId) and ships it to all ranks by any
+ * host channel (MPI_Bcast, torch.distributed, a file). */
+int misort_get_unique_id(void* id /* MISORT_UNIQUE_ID_BYTES */);
+/* Collective over all nranks processes: ncclCommInitRank. nranks must be a
+ * power of two (else MISORT_E_NOT_POW2, the reference's abort condition). */
+int misort_comm_init(misort_ctx* ctx, int nranks, int rank, const void* id);
+int misort_comm_size(misort_ctx* ctx);  /* numprocs */
+int misort_comm_rank(misort_ctx* ctx);  /* myid */
+/* psort.cc:182-196 stage schedule of `rank` in a `p`-rank hypercube: partner
+ * and keep-max flag per stage (arrays of >= 64 entries); returns the stage
+ * count d(d+1)/2 or a negative status.  Pure host logic. */
+int misort_bitonic_schedule(int p, int rank, int* partner, int* keep_max);
+/* psort.cc:556-562 block size of `rank` for n keys over p ranks. */
+int64_t misort_block_size(int64_t n, int p, int rank);
+
+/* ---- the hot path ------------------------------------------------------- */
+
+/* psort.cc:167 parallel_bitonic_sort over the context's communicator (a
+ * single rank without misort_comm_init).  d_keys holds loc_size keys of this
+ * rank's block (capacity >= loc_size); on return it holds the rank's block of
+ * the result -- the same block the reference leaves in its returned buffer,
+ * including the reference's output for uneven blocks.  max_size bounds every
+ * rank's block (psort.cc:557, the MPI_Sendrecv receive capacity).  Blocking
+ * for the host only at the start (one size exchange); the rest is enqueued on
+ * `stream`.  Steps: local sort (psort.cc:175) then d(d+1)/2 rounds of RCCL
+ * send/recv with the partner plus a device merge-split. */
+int misort_parallel_bitonic_sort(misort_ctx* ctx, int dtype, void* d_keys, int64_t loc_size,
+                                 int64_t max_size, void* stream);
+/* Same, out of place: d_in is left unchanged, d_out receives the block
+ * (d_in == d_out allowed). */
+int misort_parallel_bitonic_sort_oop(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
+                                     int64_t loc_size, int64_t max_size, void* stream);
+
+/* psort.cc:175 local ascending sort of n keys on one GPU, d_in -> d_out
+ * (d_in == d_out allowed). */
+int misort_local_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out, int64_t n,
+                      void* stream);
+
+/* Device half of compare_split_{max,min} (psort.cc:116-164) without the
+ * exchange: d_out[0..nloc) = the nloc largest (keep_max=1) or smallest
+ * (keep_max=0) keys of the sorted blocks local U recv, ascending. */
+int misort_merge_split(misort_ctx* ctx, int dtype, const void* d_local, int64_t nloc,
+                       const void* d_recv, int64_t nrecv, void* d_out, int keep_max,
+                       void* stream);
+
+/* psort.cc:497-520 check_sort: local descents of this rank's block plus the
+ * boundary descent against rank-1's last key, summed over the communicator.
+ * Synchronous; *errors is valid on every rank. */
+int misort_check_sort(misort_ctx* ctx, int dtype, const void* d_keys, int64_t n,
+                      int64_t* errors, void* stream);
+
+/* Host-buffer convenience path: h_in -> pinned staging -> device -> sort ->
+ * host h_out (this rank's block, parallel sort over the communicator).
+ * Synchronous. */
+int misort_sort_host(misort_ctx* ctx, int dtype, const void* h_in, void* h_out, int64_t loc_size,
+                     int64_t max_size);
+
+/* ---- synthetic input ------------------------------------------------------ */
+/* Counter-based SplitMix64 keys of global indices [g0, g0+n):
+ * key_g = mix(seed + (g+1)*0x9E3779B97F4A7C15), u32 = top 32 bits. */
+int misort_fill_splitmix(misort_ctx* ctx, int dtype, void* d_out, int64_t n, uint64_t seed,
+                         int64_t g0, void* stream);
+
+/* ---- per-launch profiling (HIP events around every kernel launch) ---------- */
+int misort_profile_enable(misort_ctx* ctx, int on);
+/* Reset accumulated figures. */
+int misort_profile_reset(misort_ctx* ctx);
+/* Synchronises the stream(s) used, then reports for one kernel kind: launches,
+ * summed device time (ms) and summed algorithmic HBM bytes. */
+int misort_profile_read(misort_ctx* ctx, int kind, int64_t* launches, double* total_ms,
+                        double* bytes);
+
+/* log2 of the LDS tile (keys) used for a key width of 4 or 8 bytes. */
+int misort_tile_log2(int key_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

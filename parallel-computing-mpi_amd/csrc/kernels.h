@@ -1,0 +1,59 @@
+// kernels.h -- internal launch interface of the gfx950 bitonic kernels
+// (kernels.hip).  Not part of the public C-ABI (include/misort.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace misort {
+
+// Kernel families, used for per-launch profiling (HIP events) and reporting.
+enum Kind : int {
+    KIND_TILE_SORT = 0,   // levels 1..LT inside one LDS tile
+    KIND_GLOBAL = 1,      // R fused large-stride stages, registers only
+    KIND_TILE_MERGE = 2,  // strides < tile of one level, LDS tile
+    KIND_MERGE_SPLIT = 3, // compare-split merge (keep lowest/highest n)
+    KIND_OTHER = 4,       // f64 transform, fills, checks
+    KIND_COUNT = 5
+};
+
+// Per-launch hook: called before and after every kernel launch of a sort with
+// the kernel kind and its algorithmic HBM bytes (each key read once and
+// written once).  nullptr = no profiling.
+struct LaunchHook {
+    virtual void before(Kind k, double bytes, hipStream_t s) = 0;
+    virtual void after(Kind k, hipStream_t s) = 0;
+    virtual ~LaunchHook() = default;
+};
+
+// Local ascending sort of n keys: in -> out (in == out allowed).
+// K = uint32_t or uint64_t.  ord_in: the input holds IEEE doubles that are
+// mapped to order-preserving u64 on load (K must be uint64_t); the output
+// then stays in that ordered form.
+template <typename K>
+hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, hipStream_t s,
+                      LaunchHook* hook);
+
+// Compare-split merge (device half of psort.cc:116-164): out[0..na) = the na
+// smallest (keep_max=0) or largest (keep_max=1) keys of A U B, ascending.
+// scratch must hold ceil(na/2048)+1 int64 co-ranks.
+template <typename K>
+hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
+                       int keep_max, int64_t* scratch, hipStream_t s, LaunchHook* hook);
+
+// Local descents a[i] > a[i+1] (psort.cc:497-501), compared as T
+// (uint32_t, uint64_t or double); result added to *count (device u64).
+template <typename T>
+hipError_t count_descents(const T* a, int64_t n, unsigned long long* count, hipStream_t s);
+
+// IEEE double bits <-> order-preserving u64, in place.
+hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s);
+hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s);
+
+// Counter-based SplitMix64 keys for global indices [g0, g0+n) (bench/test input).
+hipError_t fill_splitmix_u32(uint32_t* out, int64_t n, uint64_t seed, int64_t g0, hipStream_t s);
+hipError_t fill_splitmix_u64(uint64_t* out, int64_t n, uint64_t seed, int64_t g0, hipStream_t s);
+
+// Tile geometry per key type (exported for documentation/tests).
+int tile_log2(int key_bytes);
+
+}  // namespace misort

@@ -1,0 +1,270 @@
+"""misort -- MI355X-native bitonic sort (Python host mirror of the C-ABI).
+
+Mirrors the reference's sorter interface, /root/reference/Parallel-Sorting/src/
+psort.cc:
+
+* ``parallel_bitonic_sort(buffer, loc_buf_size, max_size)``   (psort.cc:167)
+* ``compare_split(local, recv, keep_max)``                    (psort.cc:116-164)
+* ``check_sort(local_numbers, local_size)``                   (psort.cc:497-520)
+* ``block_sizes(n, p)``                                       (psort.cc:556-562)
+
+with MPI ranks replaced by GPUs (one process per GPU, RCCL over xGMI) and the
+keys held in HBM as torch tensors.  Every call goes through libmisort.so
+(hand-written gfx950 HIP kernels); there is no CPU fallback: a missing
+extension raises ``NativeLibraryMissing``.
+"""
+import ctypes
+import os
+
+__all__ = [
+    "U32", "U64", "F64", "MisortError", "NotPowerOfTwo", "NativeLibraryMissing",
+    "library_path", "lib", "Context", "block_sizes", "schedule", "tile_log2",
+]
+
+U32, U64, F64 = 0, 1, 2
+KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
+_lib = None
+
+
+class MisortError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"misort error {code}: {msg}")
+        self.code = code
+
+
+class NotPowerOfTwo(MisortError):
+    """psort.cc:168-172: 'bitonic sort requires 2^d processors'."""
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def library_path():
+    return _LIB_PATH
+
+
+def lib():
+    """Load libmisort.so (built in-tree by parallel-computing-mpi_amd/csrc/Makefile)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{_LIB_PATH} not built; run `make -C parallel-computing-mpi_amd/csrc` "
+            "(or __graft_entry__.build())")
+    L = ctypes.CDLL(_LIB_PATH)
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    sig = {
+        "misort_version": ([], i32),
+        "misort_last_error": ([], ctypes.c_char_p),
+        "misort_create": ([i32, ctypes.POINTER(vp)], i32),
+        "misort_destroy": ([vp], i32),
+        "misort_stream": ([vp], vp),
+        "misort_synchronize": ([vp], i32),
+        "misort_get_unique_id": ([vp], i32),
+        "misort_comm_init": ([vp, i32, i32, vp], i32),
+        "misort_comm_size": ([vp], i32),
+        "misort_comm_rank": ([vp], i32),
+        "misort_bitonic_schedule": ([i32, i32, vp, vp], i32),
+        "misort_block_size": ([i64, i32, i32], i64),
+        "misort_parallel_bitonic_sort": ([vp, i32, vp, i64, i64, vp], i32),
+        "misort_parallel_bitonic_sort_oop": ([vp, i32, vp, vp, i64, i64, vp], i32),
+        "misort_local_sort": ([vp, i32, vp, vp, i64, vp], i32),
+        "misort_merge_split": ([vp, i32, vp, i64, vp, i64, vp, i32, vp], i32),
+        "misort_check_sort": ([vp, i32, vp, i64, ctypes.POINTER(i64), vp], i32),
+        "misort_sort_host": ([vp, i32, vp, vp, i64, i64], i32),
+        "misort_fill_splitmix": ([vp, i32, vp, i64, ctypes.c_uint64, i64, vp], i32),
+        "misort_profile_enable": ([vp, i32], i32),
+        "misort_profile_reset": ([vp], i32),
+        "misort_profile_read": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_double)], i32),
+        "misort_tile_log2": ([i32], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        msg = lib().misort_last_error().decode()
+        if rc == -2:
+            raise NotPowerOfTwo(rc, msg)
+        raise MisortError(rc, msg)
+    return rc
+
+
+def block_sizes(n, p):
+    """psort.cc:556-562 block layout."""
+    return [int(lib().misort_block_size(n, p, r)) for r in range(p)]
+
+
+def schedule(p, rank):
+    """psort.cc:182-196: [(partner, keep_max)] per stage for `rank`."""
+    partner = (ctypes.c_int * 64)()
+    keep = (ctypes.c_int * 64)()
+    s = _check(lib().misort_bitonic_schedule(p, rank, partner, keep))
+    return [(partner[i], keep[i]) for i in range(s)]
+
+
+def tile_log2(key_bytes):
+    return int(lib().misort_tile_log2(key_bytes))
+
+
+def _dtype_of(t):
+    import torch
+    m = {torch.int32: U32, torch.int64: U64, torch.float64: F64}
+    if hasattr(torch, "uint32"):
+        m[torch.uint32] = U32
+    if hasattr(torch, "uint64"):
+        m[torch.uint64] = U64
+    if t.dtype not in m:
+        raise TypeError(f"unsupported key dtype {t.dtype} (u32/u64/f64 keys)")
+    return m[t.dtype]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One GPU (HIP device) = one reference MPI rank.
+
+    ``dtype`` of a tensor selects the key type: uint32/int32 storage = u32 keys,
+    uint64/int64 storage = u64 keys (compared unsigned), float64 = f64 keys.
+    """
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        _check(lib().misort_create(device, ctypes.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().misort_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream):
+        if stream is None:
+            import torch
+            return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return ctypes.c_void_p(stream)
+
+    # ---- communicator (MPI_COMM_WORLD -> RCCL) ---------------------------------
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().misort_get_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, nranks, rank, uid):
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        _check(lib().misort_comm_init(self._h, nranks, rank, buf))
+
+    def comm_init_torch(self, group=None):
+        """Create the RCCL communicator; the id travels over torch.distributed."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        obj = [self.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        self.comm_init(world, rank, obj[0])
+
+    @property
+    def numprocs(self):
+        return int(lib().misort_comm_size(self._h))
+
+    @property
+    def myid(self):
+        return int(lib().misort_comm_rank(self._h))
+
+    # ---- hot path ---------------------------------------------------------------
+    def parallel_bitonic_sort(self, buffer, loc_buf_size=None, max_size=None, out=None,
+                              stream=None):
+        """psort.cc:167.  Sorts this rank's block `buffer[:loc_buf_size]` with the
+        reference's hypercube schedule; returns the tensor holding the result
+        (``buffer`` itself, or ``out`` when given: input left unchanged)."""
+        loc = buffer.numel() if loc_buf_size is None else int(loc_buf_size)
+        mx = loc if max_size is None else int(max_size)
+        dt = _dtype_of(buffer)
+        if out is None:
+            _check(lib().misort_parallel_bitonic_sort(self._h, dt, _ptr(buffer), loc, mx,
+                                                      self._stream(stream)))
+            return buffer
+        _check(lib().misort_parallel_bitonic_sort_oop(self._h, dt, _ptr(buffer), _ptr(out), loc,
+                                                      mx, self._stream(stream)))
+        return out
+
+    def local_sort(self, inp, out=None, n=None, stream=None):
+        """psort.cc:175 (std::sort of the local block) on the GPU."""
+        out = inp if out is None else out
+        n = inp.numel() if n is None else int(n)
+        _check(lib().misort_local_sort(self._h, _dtype_of(inp), _ptr(inp), _ptr(out), n,
+                                       self._stream(stream)))
+        return out
+
+    def compare_split(self, local, recv, keep_max, out=None, stream=None):
+        """Device half of psort.cc:116-164 (no exchange)."""
+        import torch
+        out = torch.empty_like(local) if out is None else out
+        _check(lib().misort_merge_split(self._h, _dtype_of(local), _ptr(local), local.numel(),
+                                        _ptr(recv), recv.numel(), _ptr(out), int(keep_max),
+                                        self._stream(stream)))
+        return out
+
+    def check_sort(self, local_numbers, local_size=None, stream=None):
+        """psort.cc:497-520: total error count over the communicator."""
+        n = local_numbers.numel() if local_size is None else int(local_size)
+        err = ctypes.c_int64()
+        _check(lib().misort_check_sort(self._h, _dtype_of(local_numbers), _ptr(local_numbers), n,
+                                       ctypes.byref(err), self._stream(stream)))
+        return int(err.value)
+
+    def sort_host(self, arr, max_size=None):
+        """numpy block -> pinned staging -> GPU parallel sort -> numpy."""
+        import numpy as np
+        arr = np.ascontiguousarray(arr)
+        dt = {np.dtype(np.uint32): U32, np.dtype(np.uint64): U64,
+              np.dtype(np.float64): F64}[arr.dtype]
+        out = np.empty_like(arr)
+        mx = arr.size if max_size is None else int(max_size)
+        _check(lib().misort_sort_host(self._h, dt, arr.ctypes.data_as(ctypes.c_void_p),
+                                      out.ctypes.data_as(ctypes.c_void_p), arr.size, mx))
+        return out
+
+    def fill_splitmix(self, out, seed, g0=0, stream=None):
+        _check(lib().misort_fill_splitmix(self._h, _dtype_of(out), _ptr(out), out.numel(), seed, g0,
+                                          self._stream(stream)))
+        return out
+
+    def synchronize(self):
+        _check(lib().misort_synchronize(self._h))
+
+    # ---- profiling ----------------------------------------------------------------
+    def profile(self, on=True):
+        _check(lib().misort_profile_enable(self._h, int(on)))
+
+    def profile_reset(self):
+        _check(lib().misort_profile_reset(self._h))
+
+    def profile_read(self):
+        """{kind: (launches, total_ms, algorithmic_bytes)}."""
+        res = {}
+        for k, name in enumerate(KIND_NAMES):
+            n, ms, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+            _check(lib().misort_profile_read(self._h, k, ctypes.byref(n), ctypes.byref(ms),
+                                             ctypes.byref(b)))
+            res[name] = (int(n.value), float(ms.value), float(b.value))
+        return res

@@ -1,0 +1,249 @@
+// psort -- MI355X drop-in for the reference sorter binary
+// (/root/reference/Parallel-Sorting/src/psort.cc:525-663).
+//
+//   mpirun -np P ./psort [N]
+//
+// Same command line, same generator (erand48 + ODD_DIST, psort.cc:587-614),
+// same block layout (psort.cc:556-562), same six stdout lines and the same
+// check_sort count (psort.cc:497-520) as the reference run with its bitonic
+// sort.  What changes is behind the sort entry point: each MPI rank drives one
+// GPU, keys are sorted in HBM by libmisort (gfx950 kernels) and the
+// compare-split exchange runs over RCCL/xGMI instead of MPI_Sendrecv.  MPI is
+// kept only for process bootstrap, the generator's seed hand-off, timing
+// reductions and the RCCL id broadcast.
+//
+// Timed region ("parallel sort time", psort.cc:633-656): keys resident in HBM,
+// barrier, sort, stream sync, max over ranks.  The host<->device copies are
+// reported separately with --verbose.
+//
+// Extensions (not in the reference; off by default):
+//   --keys FILE --dtype u32|u64|f64   sort a raw little-endian key file
+//   --out FILE                        write the rank-ordered result
+//   --verbose                         extra timing lines on stderr
+#include <mpi.h>
+
+#include <fcntl.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "misort.h"
+
+using std::cout;
+using std::endl;
+
+static int numprocs, myid;  // psort.cc:107
+
+// psort.cc:25-65: signal traps and the 9-minute watchdog.
+static void program_trap(int sig) {
+    const char* t = "(undefined)";
+    switch (sig) {
+        case SIGBUS: t = "a Bus Error"; break;
+        case SIGSEGV: t = "a Segmentation Violation"; break;
+        case SIGILL: t = "an Illegal Instruction Call"; break;
+        case SIGSYS: t = "an Illegal System Call"; break;
+        case SIGFPE: t = "a Floating Point Exception"; break;
+        case SIGALRM: t = "a Alarm Signal!"; break;
+    }
+    fprintf(stderr, "ERROR: Program terminated due to %s\n", t);
+    abort();
+}
+static void chopsigs(unsigned seconds) {
+    for (int s : {SIGBUS, SIGSEGV, SIGILL, SIGSYS, SIGFPE, SIGALRM}) signal(s, program_trap);
+    alarm(seconds);
+}
+
+// psort.cc:68-75
+static double get_timer() {
+    static double to = 0;
+    double tn = MPI_Wtime(), t = tn - to;
+    to = tn;
+    return t;
+}
+
+#define HIP_OK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                 \
+            MPI_Abort(MPI_COMM_WORLD, -1);                                          \
+        }                                                                           \
+    } while (0)
+
+static void misort_ok(int rc, const char* what) {
+    if (rc == MISORT_E_NOT_POW2) {  // psort.cc:168-172
+        std::cerr << "bitonic sort requires 2^d processors" << endl;
+        MPI_Abort(MPI_COMM_WORLD, -1);
+        abort();
+    }
+    if (rc != 0) {
+        fprintf(stderr, "%s: %s\n", what, misort_last_error());
+        MPI_Abort(MPI_COMM_WORLD, -1);
+    }
+}
+
+// psort.cc:587-609 with the rank-to-rank seed chain replaced by an LCG
+// jump-ahead to the block's global offset (same values for every P), split
+// over host threads.
+static const uint64_t A48 = 0x5DEECE66DULL, C48 = 0xB, M48 = (1ULL << 48) - 1;
+static uint64_t lcg_skip(uint64_t x, uint64_t k) {
+    uint64_t aa = 1, cc = 0, a = A48, c = C48;
+    while (k) {
+        if (k & 1) { aa = (aa * a) & M48; cc = (cc * a + c) & M48; }
+        c = (c * a + c) & M48;
+        a = (a * a) & M48;
+        k >>= 1;
+    }
+    return (aa * x + cc) & M48;
+}
+static void generate(long long n, long long g0, long long cnt, double* out) {
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency() / std::max(1, numprocs)));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) {
+        th.emplace_back([=] {
+            long long b = cnt * t / nt, e = cnt * (t + 1) / nt;
+            uint64_t x = lcg_skip(1ULL << 32, (uint64_t)(g0 + b));
+            for (long long k = b; k < e; ++k) {
+                unsigned short ctr = (unsigned short)((g0 + k + 1) & 0xFFFF);  // xi[3] += 1
+                x = (A48 * x + C48) & M48;                                    // erand48
+                double val = ldexp((double)x, -48);
+                double p = double(ctr) / double(n);                           // ODD_DIST
+                val = pow(val, 1.0 + 3 * p);
+                out[k] = val * val;
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+}
+
+int main(int argc, char** argv) {
+    MPI_Init(&argc, &argv);
+    chopsigs(540);
+    MPI_Comm_size(MPI_COMM_WORLD, &numprocs);
+    MPI_Comm_rank(MPI_COMM_WORLD, &myid);
+
+    long long input_size = 1024;  // psort.cc:538
+    std::string keys_file, out_file, dtype_s = "f64";
+    bool verbose = false;
+    if (argc == 2) input_size = atoll(argv[1]);  // psort.cc:541-544
+    for (int a = 1; a < argc && argc > 2; ++a) {
+        std::string s = argv[a];
+        if (s == "--keys" && a + 1 < argc) keys_file = argv[++a];
+        else if (s == "--out" && a + 1 < argc) out_file = argv[++a];
+        else if (s == "--dtype" && a + 1 < argc) dtype_s = argv[++a];
+        else if (s == "--verbose") verbose = true;
+        else if (s[0] != '-') input_size = atoll(s.c_str());
+    }
+    const int dtype = dtype_s == "u32" ? MISORT_U32 : dtype_s == "u64" ? MISORT_U64 : MISORT_F64;
+    const size_t w = dtype == MISORT_U32 ? 4 : 8;
+    int fd = -1;
+    if (!keys_file.empty()) {
+        fd = open(keys_file.c_str(), O_RDONLY);
+        if (fd < 0) { perror(keys_file.c_str()); MPI_Abort(MPI_COMM_WORLD, 2); }
+        input_size = (long long)(lseek(fd, 0, SEEK_END) / (off_t)w);
+    }
+
+    if (myid == 0) {  // psort.cc:547-551
+        cout << "Starting " << numprocs << " processors." << endl;
+        cout << "generating input sequence consisting of " << input_size << " doubles." << endl;
+    }
+
+    // psort.cc:556-562
+    long long local_input_size = input_size / numprocs;
+    const long long max_local_size = local_input_size + 1;
+    const long long remainder = input_size % numprocs;
+    if (myid < remainder) local_input_size += 1;
+    const long long offset = (input_size / numprocs) * myid + (myid < remainder ? myid : remainder);
+
+    // One GPU per rank; RCCL communicator in place of MPI_COMM_WORLD.
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    const char* dev_env = getenv("PSORT_DEVICE");
+    const int dev = dev_env ? atoi(dev_env) : myid % std::max(1, ndev);
+    misort_ctx* ctx = nullptr;
+    misort_ok(misort_create(dev, &ctx), "misort_create");
+    if (numprocs > 1) {
+        unsigned char id[MISORT_UNIQUE_ID_BYTES];
+        if (myid == 0) misort_ok(misort_get_unique_id(id), "misort_get_unique_id");
+        MPI_Bcast(id, sizeof id, MPI_BYTE, 0, MPI_COMM_WORLD);
+        misort_ok(misort_comm_init(ctx, numprocs, myid, id), "misort_comm_init");
+    }
+
+    std::vector<unsigned char> host((size_t)max_local_size * w + 8);
+    MPI_Barrier(MPI_COMM_WORLD);  // psort.cc:569
+    get_timer();
+    if (fd >= 0) {
+        if (local_input_size > 0 &&
+            pread(fd, host.data(), (size_t)local_input_size * w, (off_t)(offset * (long long)w)) !=
+                (ssize_t)(local_input_size * w)) {
+            fprintf(stderr, "short read\n");
+            MPI_Abort(MPI_COMM_WORLD, 2);
+        }
+        close(fd);
+    } else {
+        generate(input_size, offset, local_input_size, (double*)host.data());
+    }
+    MPI_Barrier(MPI_COMM_WORLD);  // psort.cc:617
+    double seq_gen_time = get_timer(), max_time = 0;
+    MPI_Reduce(&seq_gen_time, &max_time, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+    if (myid == 0) {  // psort.cc:626-631
+        cout << "completed generation of a sequence of size " << input_size << "." << endl;
+        cout << "sequence generation required " << max_time << " seconds." << endl;
+    }
+
+    hipStream_t st = (hipStream_t)misort_stream(ctx);
+    void* d_keys = nullptr;
+    HIP_OK(hipMalloc(&d_keys, std::max<size_t>(16, (size_t)max_local_size * w)));
+    double t_h2d = MPI_Wtime();
+    HIP_OK(hipMemcpyAsync(d_keys, host.data(), (size_t)local_input_size * w, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    t_h2d = MPI_Wtime() - t_h2d;
+
+    MPI_Barrier(MPI_COMM_WORLD);  // psort.cc:633
+    get_timer();
+    misort_ok(misort_parallel_bitonic_sort(ctx, dtype, d_keys, local_input_size, max_local_size, st),
+              "parallel_bitonic_sort");
+    HIP_OK(hipStreamSynchronize(st));
+    double par_sort_time = get_timer();  // psort.cc:650-656
+    MPI_Reduce(&par_sort_time, &max_time, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+    if (myid == 0) cout << "parallel sort time = " << max_time << endl;
+
+    int64_t errors = 0;  // psort.cc:659 -> 497-520
+    misort_ok(misort_check_sort(ctx, dtype, d_keys, local_input_size, &errors, st), "check_sort");
+    if (myid == 0) cout << errors << " errors in sorting" << endl;
+
+    if (!out_file.empty() || verbose) {
+        double t_d2h = MPI_Wtime();
+        HIP_OK(hipMemcpyAsync(host.data(), d_keys, (size_t)local_input_size * w, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        t_d2h = MPI_Wtime() - t_d2h;
+        if (!out_file.empty()) {
+            int ofd = open(out_file.c_str(), O_WRONLY | O_CREAT, 0644);
+            if (ofd < 0 || (local_input_size > 0 &&
+                            pwrite(ofd, host.data(), (size_t)local_input_size * w,
+                                   (off_t)(offset * (long long)w)) != (ssize_t)(local_input_size * w))) {
+                perror(out_file.c_str());
+                MPI_Abort(MPI_COMM_WORLD, 2);
+            }
+            close(ofd);
+        }
+        if (verbose)
+            fprintf(stderr, "rank %d device %d: %lld keys, h2d %.6f s, d2h %.6f s\n", myid, dev,
+                    local_input_size, t_h2d, t_d2h);
+    }
+    HIP_OK(hipFree(d_keys));
+    misort_destroy(ctx);
+    MPI_Finalize();
+    return 0;
+}
