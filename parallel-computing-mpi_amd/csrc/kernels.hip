@@ -12,19 +12,19 @@
 // sentinel (all-ones) suffix can only move upwards, so the padding of n up to a
 // power of two is VIRTUAL: indices >= n read as all-ones and are never stored.
 //
-// Three kernel families sweep the network:
-//   k_tile_sort   levels 1..LT of one 2^LT-key tile held in LDS (64 KiB);
-//   k_global_pass R (<=5) consecutive large strides of one level, fused in
-//                 registers: each lane holds 2^R rows x one 16-byte vector,
-//                 every row a fully coalesced 1 KiB wave access;
-//   k_tile_merge  the strides < 2^LT of one level, in an LDS tile.
-// Inside an LDS tile a "phase" gives each lane the 32 keys that differ only in a
-// 5-bit window [b, b+5) of the index; the phase's stages run in registers and
-// the XOR swizzle phys(i) = i ^ ((i >> 5) & 31) keeps every ds_read/ds_write of
-// a phase bank-conflict free for all windows.
+// Passes over HBM (each moves every key once in and once out):
+//   k_stream<SORT>   levels 1..LT of every 2^LT-key tile (LDS, 64 KiB + pad);
+//   k_stream<ROWS>   up to 9 consecutive large strides of one level: a tile is
+//                    2^R rows at the stride distance times 2^(LT-R) consecutive
+//                    keys, so every row segment is a coalesced >= 128 B run;
+//   k_stream<MERGE>  the strides < 2^LT of one level, in an LDS tile;
+//   k_global_pass    (optional, MISORT_REGPASS) register-only large strides.
+// All of them share one persistent, register-prefetching tile engine.
 //
 // A pass over 2^k keys moves 2 * 2^k * sizeof(K) algorithmic HBM bytes.
 #include "kernels.h"
+
+#include <stdlib.h>
 
 namespace misort {
 namespace {
@@ -35,8 +35,7 @@ template <>
 struct KT<uint32_t> {
     static constexpr uint32_t MAX = 0xFFFFFFFFu;
     static constexpr int V = 4;     // keys per 16-byte vector
-    static constexpr int LT = 14;   // log2 keys per LDS tile (64 KiB)
-    static constexpr int NT = 512;  // tile workgroup: 32 keys per lane
+    static constexpr int LT = 14;   // log2 keys per LDS tile (64 KiB + padding)
     typedef uint32_t vec __attribute__((ext_vector_type(4)));
 };
 template <>
@@ -44,11 +43,11 @@ struct KT<uint64_t> {
     static constexpr uint64_t MAX = ~0ull;
     static constexpr int V = 2;
     static constexpr int LT = 13;
-    static constexpr int NT = 256;
     typedef uint64_t vec __attribute__((ext_vector_type(2)));
 };
 
-constexpr int RMAX = 5;         // strides fused per global pass
+constexpr int RMAX = 5;         // strides fused per register-only global pass
+constexpr int RMAX_ROWS = 9;    // strides fused per ROWS (LDS) pass
 constexpr int GP_THREADS = 256; // global-pass workgroup
 
 __device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
@@ -100,131 +99,6 @@ __device__ __forceinline__ void store_vec(K* __restrict__ p, int64_t i0, int64_t
         for (int j = 0; j < V; ++j)
             if (i0 + j < n) p[i0 + j] = w[j];
     }
-}
-
-__device__ __forceinline__ int phys(int i) { return i ^ ((i >> 5) & 31); }
-
-// Stages of one phase on the 32 keys of a lane.  Relative stride bits
-// top, top-1, .., top-cnt+1; the first is the flip stage when `flip`.
-// top/cnt/flip are wave-uniform, so the guards are scalar branches.
-template <typename K>
-__device__ __forceinline__ void reg_stages(K (&v)[32], int top, int cnt, bool flip) {
-#pragma unroll
-    for (int r = 4; r >= 0; --r) {
-        if (r > top || r <= top - cnt) continue;
-        if (flip && r == top) {
-#pragma unroll
-            for (int c = 0; c < 32; ++c)
-                if (!(c & (1 << r))) cx(v[c], v[c ^ ((2 << r) - 1)]);
-        } else {
-#pragma unroll
-            for (int c = 0; c < 32; ++c)
-                if (!(c & (1 << r))) cx(v[c], v[c | (1 << r)]);
-        }
-    }
-}
-
-// One LDS phase with index window [b, b+5).  The lane's other index bits are
-// its thread id.  For a flip phase the keys whose window bit `top` is set take
-// the mirrored low bits (below b), so each lane holds both halves of every
-// mirror pair.
-template <typename K>
-__device__ __forceinline__ void lds_phase(K* s, int t, int b, int top, int cnt, bool flip) {
-    const int lowm = (1 << b) - 1;
-    const int tl = t & lowm;
-    const int th = (t >> b) << (b + 5);
-    const int tlm = flip ? (tl ^ lowm) : tl;
-    K v[32];
-#pragma unroll
-    for (int c = 0; c < 32; ++c) {
-        const int l = ((c >> top) & 1) ? tlm : tl;
-        v[c] = s[phys(th | (c << b) | l)];
-    }
-    reg_stages(v, top, cnt, flip);
-#pragma unroll
-    for (int c = 0; c < 32; ++c) {
-        const int l = ((c >> top) & 1) ? tlm : tl;
-        s[phys(th | (c << b) | l)] = v[c];
-    }
-}
-
-// Half-cleaner strides hi..0 of a level (or the flip first when `flip`).
-template <typename K>
-__device__ __forceinline__ void lds_strides(K* s, int t, int hi, bool flip) {
-    while (hi >= 0) {
-        const int b = hi > 4 ? hi - 4 : 0;
-        lds_phase<K>(s, t, b, hi - b, hi - b + 1, flip);
-        __syncthreads();
-        flip = false;
-        hi = b - 1;
-    }
-}
-
-template <typename K, bool ORD>
-__device__ __forceinline__ void tile_load(K* s, const K* __restrict__ src, int64_t base,
-                                          int64_t n, int t) {
-    constexpr int LT = KT<K>::LT, NT = KT<K>::NT, V = KT<K>::V;
-#pragma unroll
-    for (int k = 0; k < (1 << LT) / (NT * V); ++k) {
-        const int e = (k * NT + t) * V;
-        K w[V];
-        load_vec<K, ORD>(src, base + e, n, w);
-#pragma unroll
-        for (int j = 0; j < V; ++j) s[phys(e + j)] = w[j];
-    }
-}
-
-template <typename K>
-__device__ __forceinline__ void tile_store(const K* s, K* __restrict__ dst, int64_t base,
-                                           int64_t n, int t) {
-    constexpr int LT = KT<K>::LT, NT = KT<K>::NT, V = KT<K>::V;
-#pragma unroll
-    for (int k = 0; k < (1 << LT) / (NT * V); ++k) {
-        const int e = (k * NT + t) * V;
-        K w[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) w[j] = s[phys(e + j)];
-        store_vec<K>(dst, base + e, n, w);
-    }
-}
-
-// Levels 1..LT of the tile starting at blockIdx.x << LT: sorted ascending runs
-// of 2^LT keys (the last run holds min(n - base, 2^LT) real keys).
-template <typename K, bool ORD>
-__global__ __launch_bounds__(KT<K>::NT) void k_tile_sort(const K* __restrict__ in,
-                                                          K* __restrict__ out, int64_t n) {
-    constexpr int LT = KT<K>::LT;
-    __shared__ K s[1 << LT];
-    const int t = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x << LT;
-    tile_load<K, ORD>(s, in, base, n, t);
-    __syncthreads();
-    {   // levels 1..5: window [0,5), 32 consecutive keys per lane
-        K v[32];
-#pragma unroll
-        for (int c = 0; c < 32; ++c) v[c] = s[phys((t << 5) | c)];
-#pragma unroll
-        for (int m = 1; m <= 5; ++m) reg_stages(v, m - 1, m, true);
-#pragma unroll
-        for (int c = 0; c < 32; ++c) s[phys((t << 5) | c)] = v[c];
-    }
-    __syncthreads();
-    for (int m = 6; m <= LT; ++m) lds_strides<K>(s, t, m - 1, true);
-    tile_store<K>(s, out, base, n, t);
-}
-
-// Strides 2^(LT-1) .. 1 of a level m > LT, in place.
-template <typename K>
-__global__ __launch_bounds__(KT<K>::NT) void k_tile_merge(K* __restrict__ a, int64_t n) {
-    constexpr int LT = KT<K>::LT;
-    __shared__ K s[1 << LT];
-    const int t = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x << LT;
-    if (base >= n) return;
-    tile_load<K, false>(s, a, base, n, t);
-    __syncthreads();
-    lds_strides<K>(s, t, LT - 1, false);
-    tile_store<K>(s, a, base, n, t);
 }
 
 // Wave-uniform global pointer: readfirstlane pins it in SGPRs, so a row access
@@ -311,6 +185,267 @@ __global__ __launch_bounds__(GP_THREADS) void k_global_pass(K* __restrict__ a, i
 #pragma unroll
             for (int j = 0; j < V; ++j) x[j] = w[j];
             gstore<vec>(rowp + (mir ? boffm : boff), x);
+        }
+    }
+}
+
+// ------------------------------------------------- streaming tile engine
+//
+// Persistent workgroups walk a list of 2^LT-key tiles.  While the LDS phases of
+// tile i run, the 16-byte loads of tile i+1 are already in flight into a
+// register buffer, so HBM streams continuously with 2 workgroups per CU.
+//
+// A tile is a set of 2^LT keys that one network segment touches only among
+// themselves, addressed through a "virtual" index v in [0, 2^LT):
+//   CONTIG   v -> tile*2^LT + v                       (tile sort / tile merge)
+//   ROWS     v = (c << logB) | j -> wbase + (c << lo) + low(c) + j
+//            2^R rows c at global stride 2^lo (the R strides 2^hi..2^lo of one
+//            level, R = LT - logB) times B = 2^logB consecutive keys.  For the
+//            first pass of a level (flip), rows whose top bit is set start at
+//            the mirrored block 2^lo - L0 - B, which turns the level's global
+//            flip i <-> i ^ (2^(hi+1) - 1) into the tile's own flip v <-> ~v.
+//
+// Register slots: lane t loads LOADS = 32/V vectors, slot k = virtual keys
+// (k*NT + t)*V .. +V-1, so the top KB = log2(LOADS) virtual bits are the slot
+// index and the bottom VB = log2(V) bits the vector component.  Strides on
+// those bits run in registers before the LDS write (slots) and after the LDS
+// read (components); only the strides in between cost an LDS phase.  For a
+// flip on the top slot bit the upper slots load the mirrored lane's vector
+// reversed, so every mirror pair meets in one lane at one component.
+//
+// LDS layout: key v at word v + v/32.  The padding keeps every phase's
+// 32-lane accesses on distinct banks, and since v + v/32 is additive over
+// disjoint bit fields every access is one base VGPR plus an immediate offset.
+enum TileMode : int { TM_SORT = 0, TM_MERGE = 1, TM_ROWS = 2 };
+
+struct TileMap {
+    int64_t ntiles;  // real tiles (a prefix of the tile list)
+    int lo, hi, logB, flip;
+};
+
+template <typename K, int LT>
+struct TileGeo {
+    static constexpr int T = 1 << LT, NT = T / 32, V = KT<K>::V, LOADS = T / (NT * V);
+    static constexpr int KB = LOADS == 16 ? 4 : LOADS == 8 ? 3 : LOADS == 4 ? 2 : 1;
+    static constexpr int VB = V == 4 ? 2 : 1;
+};
+
+__host__ __device__ constexpr int pad(int v) { return v + (v >> 5); }
+
+template <int LT, int MODE>
+__device__ __forceinline__ int64_t tile_index(const TileMap& m, int64_t tile, int e) {
+    if constexpr (MODE != TM_ROWS) {
+        return (tile << LT) + e;
+    } else {
+        const int R = LT - m.logB;
+        const int sh = m.lo - m.logB;  // log2 tiles per 2^(hi+1) segment
+        const int64_t seg = tile >> sh, lb = tile & (((int64_t)1 << sh) - 1);
+        const int64_t L0 = lb << m.logB;
+        const int c = e >> m.logB, j = e & ((1 << m.logB) - 1);
+        const bool mir = m.flip && ((c >> (R - 1)) & 1);
+        const int64_t low = mir ? (((int64_t)1 << m.lo) - L0 - ((int64_t)1 << m.logB)) : L0;
+        return (seg << (m.hi + 1)) + ((int64_t)c << m.lo) + low + j;
+    }
+}
+
+// Every key of the tile lies below n (then no per-element bounds checks).
+template <int LT, int MODE>
+__device__ __forceinline__ bool tile_full(const TileMap& m, int64_t tile, int64_t n) {
+    if constexpr (MODE != TM_ROWS) {
+        return ((tile + 1) << LT) <= n;
+    } else {
+        return (((tile >> (m.lo - m.logB)) + 1) << (m.hi + 1)) <= n;
+    }
+}
+
+// Slot k of lane t: virtual vector start, and whether it is held mirrored.
+template <typename K, int LT, bool MIRROR>
+__device__ __forceinline__ int slot_lane(int k, int t) {
+    typedef TileGeo<K, LT> G;
+    return (MIRROR && k >= G::LOADS / 2) ? (G::NT - 1 - t) : t;
+}
+
+template <typename K, int LT, int MODE, bool MIRROR, bool ORD>
+__device__ __forceinline__ void tile_fetch(K (*pre)[KT<K>::V], const K* src, const TileMap& m,
+                                           int64_t tile, int64_t n, int t) {
+    typedef TileGeo<K, LT> G;
+    const bool full = tile_full<LT, MODE>(m, tile, n);
+#pragma unroll
+    for (int k = 0; k < G::LOADS; ++k) {
+        const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+        const int64_t gi = tile_index<LT, MODE>(m, tile, e);
+        typename KT<K>::vec x;
+        if (full) {
+            x = *reinterpret_cast<const typename KT<K>::vec*>(src + gi);
+            if constexpr (ORD) {
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) x[j] = ord_of_f64(x[j]);
+            }
+        } else {
+            K w[G::V];
+            load_vec<K, ORD>(src, gi, n, w);
+#pragma unroll
+            for (int j = 0; j < G::V; ++j) x[j] = w[j];
+        }
+        const bool mk = MIRROR && k >= G::LOADS / 2;
+#pragma unroll
+        for (int j = 0; j < G::V; ++j) pre[k][j] = mk ? x[G::V - 1 - j] : x[j];
+    }
+}
+
+template <typename K, int LT, int MODE>
+__device__ __forceinline__ void store_slot(K* dst, const TileMap& m, int64_t tile, int64_t n,
+                                           bool full, int e, const K (&w)[KT<K>::V]) {
+    const int64_t gi = tile_index<LT, MODE>(m, tile, e);
+    if (full) {
+        typename KT<K>::vec x;
+#pragma unroll
+        for (int j = 0; j < KT<K>::V; ++j) x[j] = w[j];
+        *reinterpret_cast<typename KT<K>::vec*>(dst + gi) = x;
+    } else {
+        store_vec<K>(dst, gi, n, w);
+    }
+}
+
+// Compile-time stage list on 32 register keys: relative bits TOP..TOP-CNT+1.
+template <typename K, int TOP, int CNT, bool FLIP>
+__device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
+#pragma unroll
+    for (int r = TOP; r > TOP - CNT; --r) {
+        const bool fl = FLIP && r == TOP;
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (!(c & (1 << r))) cx(v[c], v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))]);
+    }
+}
+
+// One LDS phase, window [B, B+5) of the virtual index, compile-time shape.
+template <typename K, int B, int TOP, int CNT, bool FLIP>
+__device__ __forceinline__ void phase_c(K* s, int t) {
+    constexpr int lowm = (1 << B) - 1;
+    const int tl = t & lowm;
+    const int th = (t >> B) << (B + 5);
+    const int a0 = pad(th | tl);
+    const int a1 = FLIP ? pad(th | (tl ^ lowm)) : a0;
+    K v[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) v[c] = s[(((c >> TOP) & 1) ? a1 : a0) + pad(c << B)];
+    reg_stages_c<K, TOP, CNT, FLIP>(v);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) s[(((c >> TOP) & 1) ? a1 : a0) + pad(c << B)] = v[c];
+}
+
+// Strides HI..STOP of the virtual index through LDS phases (flip first).
+template <typename K, int HI, int STOP, bool FLIP>
+__device__ __forceinline__ void lds_range(K* s, int t) {
+    if constexpr (HI >= STOP) {
+        constexpr int B = HI > 4 ? HI - 4 : 0;
+        constexpr int LOWEST = B > STOP ? B : STOP;
+        phase_c<K, B, HI - B, HI - LOWEST + 1, FLIP>(s, t);
+        __syncthreads();
+        lds_range<K, LOWEST - 1, STOP, false>(s, t);
+    }
+}
+
+// Levels L..LT of the tile sort (level 1..5 done by the caller).
+template <typename K, int L, int LT>
+__device__ __forceinline__ void sort_levels(K* s, int t) {
+    if constexpr (L <= LT) {
+        lds_range<K, L - 1, 0, true>(s, t);
+        sort_levels<K, L + 1, LT>(s, t);
+    }
+}
+
+template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD>
+__global__ __launch_bounds__((TileGeo<K, LT>::NT), (2 * TileGeo<K, LT>::NT / 256)) void k_stream(
+    const K* in, K* out, int64_t n, TileMap m) {
+    typedef TileGeo<K, LT> G;
+    constexpr bool MIRROR = MODE == TM_ROWS && FLIP;
+    // slot-bit strides done in registers before the LDS write
+    constexpr int PRE = MODE == TM_MERGE ? G::KB : MODE == TM_ROWS ? (R < G::KB ? R : G::KB) : 0;
+    __shared__ K s[pad(G::T)];
+    const int t = threadIdx.x;
+    K pre[G::LOADS][G::V];
+    int64_t tile = blockIdx.x;
+    if (tile >= m.ntiles) return;
+    tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, tile, n, t);
+    for (; tile < m.ntiles; tile += gridDim.x) {
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) {
+            const int r = G::KB - 1 - i;
+            const bool fl = MIRROR && i == 0;
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                if (k & (1 << r)) continue;
+                const int p = fl ? (k ^ (G::LOADS - 1)) : (k | (1 << r));
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) cx(pre[k][j], pre[p][j]);
+            }
+        }
+        const bool full = tile_full<LT, MODE>(m, tile, n);
+        if constexpr (MODE == TM_ROWS && R <= G::KB) {
+            // every stride of this pass was a slot bit: store straight from registers
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                K w[G::V];
+                const bool mk = MIRROR && k >= G::LOADS / 2;
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) w[j] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
+                store_slot<K, LT, MODE>(out, m, tile, n, full,
+                                        (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V, w);
+            }
+            const int64_t nxt = tile + gridDim.x;
+            if (nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+        } else {
+            // registers -> LDS (mirrored slots to their own virtual position)
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                const bool mk = MIRROR && k >= G::LOADS / 2;
+                const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) s[pad(e + j)] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
+            }
+            __syncthreads();
+            const int64_t nxt = tile + gridDim.x;
+            if (nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+            if constexpr (MODE == TM_SORT) {
+                {   // levels 1..5: window [0,5), 32 consecutive keys per lane
+                    K v[32];
+                    const int a0 = pad(t << 5);
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) v[c] = s[a0 + c];
+                    reg_stages_c<K, 0, 1, true>(v);
+                    reg_stages_c<K, 1, 2, true>(v);
+                    reg_stages_c<K, 2, 3, true>(v);
+                    reg_stages_c<K, 3, 4, true>(v);
+                    reg_stages_c<K, 4, 5, true>(v);
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) s[a0 + c] = v[c];
+                }
+                __syncthreads();
+                sort_levels<K, 6, LT>(s, t);
+            } else if constexpr (MODE == TM_MERGE) {
+                lds_range<K, LT - G::KB - 1, G::VB, false>(s, t);
+            } else {
+                lds_range<K, LT - G::KB - 1, LT - R, false>(s, t);
+            }
+            // LDS -> registers -> HBM; in a merge the vector-component strides run here
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                const int e = (k * G::NT + t) * G::V;
+                K w[G::V];
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) w[j] = s[pad(e + j)];
+                if constexpr (MODE == TM_MERGE) {
+#pragma unroll
+                    for (int r = G::VB - 1; r >= 0; --r)
+#pragma unroll
+                        for (int j = 0; j < G::V; ++j)
+                            if (!(j & (1 << r))) cx(w[j], w[j | (1 << r)]);
+                }
+                store_slot<K, LT, MODE>(out, m, tile, n, full, e, w);
+            }
+            __syncthreads();
         }
     }
 }
@@ -480,36 +615,112 @@ void launch_global_r(int r, bool flip, K* a, int64_t n, int hi, int k, hipStream
 
 int tile_log2(int key_bytes) { return key_bytes == 4 ? KT<uint32_t>::LT : KT<uint64_t>::LT; }
 
+namespace {
+
+// Pass-planner knobs (environment, read once): MISORT_RMAX = most strides one
+// ROWS pass fuses (default 9), MISORT_REGPASS = largest stride count that uses
+// the register-only pass instead (default 0 = never).
+struct PlanKnobs {
+    int rmax = RMAX_ROWS, regpass = 0;
+    PlanKnobs() {
+        if (const char* e = getenv("MISORT_RMAX")) rmax = atoi(e) < 1 ? 1 : atoi(e);
+        if (rmax > RMAX_ROWS) rmax = RMAX_ROWS;
+        if (const char* e = getenv("MISORT_REGPASS")) regpass = atoi(e);
+        if (regpass > RMAX) regpass = RMAX;
+    }
+};
+const PlanKnobs& knobs() {
+    static PlanKnobs k;
+    return k;
+}
+
+template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD>
+void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
+    typedef TileGeo<K, LT> G;
+    static int64_t cap = 0;  // resident workgroups for this instantiation
+    if (cap == 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_stream<K, LT, MODE, R, FLIP, ORD>,
+                                                           G::NT, 0);
+        cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
+    }
+    const int64_t grid = m.ntiles < cap ? m.ntiles : cap;
+    if (grid > 0) k_stream<K, LT, MODE, R, FLIP, ORD><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
+}
+
+template <typename K, int R>
+void launch_rows_r(K* a, int64_t n, const TileMap& m, hipStream_t s) {
+    constexpr int LT = KT<K>::LT;
+    if (m.flip) launch_stream<K, LT, TM_ROWS, R, true, false>(a, a, n, m, s);
+    else launch_stream<K, LT, TM_ROWS, R, false, false>(a, a, n, m, s);
+}
+
+// One ROWS pass: strides 2^hi .. 2^(hi-R+1) of a level over 2^k (virtual) keys.
+template <typename K>
+void launch_rows(K* a, int64_t n, int hi, int R, bool flip, hipStream_t s) {
+    constexpr int LT = KT<K>::LT;
+    TileMap m{};
+    m.lo = hi - R + 1;
+    m.hi = hi;
+    m.logB = LT - R;
+    m.flip = flip;
+    const int64_t per_seg = ((int64_t)1 << m.lo) >> m.logB;
+    const int64_t full_segs = n >> (hi + 1);
+    const int64_t rem = n - (full_segs << (hi + 1));
+    int64_t part = (rem + ((int64_t)1 << m.logB) - 1) >> m.logB;
+    if (part > per_seg) part = per_seg;
+    m.ntiles = full_segs * per_seg + part;
+    switch (R) {
+        case 1: launch_rows_r<K, 1>(a, n, m, s); break;
+        case 2: launch_rows_r<K, 2>(a, n, m, s); break;
+        case 3: launch_rows_r<K, 3>(a, n, m, s); break;
+        case 4: launch_rows_r<K, 4>(a, n, m, s); break;
+        case 5: launch_rows_r<K, 5>(a, n, m, s); break;
+        case 6: launch_rows_r<K, 6>(a, n, m, s); break;
+        case 7: launch_rows_r<K, 7>(a, n, m, s); break;
+        case 8: launch_rows_r<K, 8>(a, n, m, s); break;
+        default: launch_rows_r<K, 9>(a, n, m, s); break;
+    }
+}
+
+}  // namespace
+
 template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, hipStream_t s,
                       LaunchHook* hook) {
-    constexpr int LT = KT<K>::LT, NT = KT<K>::NT;
+    constexpr int LT = KT<K>::LT;
     if (n <= 0) return hipSuccess;
     const int k = ceil_log2(n);
-    const unsigned tiles = (unsigned)((n + (1 << LT) - 1) >> LT);
     const double pass_bytes = 2.0 * (double)n * sizeof(K);
+    TileMap tm{};
+    tm.ntiles = (n + (1 << LT) - 1) >> LT;
     {
         HookScope hs(hook, KIND_TILE_SORT, pass_bytes, s);
         if constexpr (sizeof(K) == 8) {
-            if (ord_in) k_tile_sort<K, true><<<tiles, NT, 0, s>>>(in, out, n);
-            else k_tile_sort<K, false><<<tiles, NT, 0, s>>>(in, out, n);
+            if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(in, out, n, tm, s);
+            else launch_stream<K, LT, TM_SORT, 0, false, false>(in, out, n, tm, s);
         } else {
             if (ord_in) return hipErrorInvalidValue;
-            k_tile_sort<K, false><<<tiles, NT, 0, s>>>(in, out, n);
+            launch_stream<K, LT, TM_SORT, 0, false, false>(in, out, n, tm, s);
         }
     }
+    const PlanKnobs& kn = knobs();
     for (int m = LT + 1; m <= k; ++m) {
+        // strides 2^(m-1) .. 2^LT split into near-equal passes of <= rmax
+        const int x = m - LT;
+        const int parts = (x + kn.rmax - 1) / kn.rmax;
         int hi = m - 1;
-        bool first = true;
-        while (hi >= LT) {
-            const int r = hi - LT + 1 < RMAX ? hi - LT + 1 : RMAX;
+        for (int p = 0; p < parts; ++p) {
+            const int R = x / parts + (p < x % parts ? 1 : 0);
             HookScope hs(hook, KIND_GLOBAL, pass_bytes, s);
-            launch_global_r<K>(r, first, out, n, hi, k, s);
-            hi -= r;
-            first = false;
+            if (R <= kn.regpass) launch_global_r<K>(R, p == 0, out, n, hi, k, s);
+            else launch_rows<K>(out, n, hi, R, p == 0, s);
+            hi -= R;
         }
         HookScope hs(hook, KIND_TILE_MERGE, pass_bytes, s);
-        k_tile_merge<K><<<tiles, NT, 0, s>>>(out, n);
+        launch_stream<K, LT, TM_MERGE, 0, false, false>(out, out, n, tm, s);
     }
     return hipGetLastError();
 }
