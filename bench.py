@@ -149,6 +149,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    ctx.exchange_stats()  # reset
     events = not args.no_kernel_events
     if events:
         ctx.profile(True)
@@ -163,6 +164,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern = ctx.profile_read() if events else {}
     ctx.profile(False)
+    xst = ctx.exchange_stats()
 
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -191,6 +193,10 @@ def main():
                        "parallelism": f"hypercube bitonic, {world} GPU(s), RCCL compare-split"},
             "check_errors": errors,
         }
+        if world > 1:
+            out["exchange"] = {"stages_per_step": xst[0] / args.steps,
+                               "rank0_bytes_per_step": xst[1] / args.steps,
+                               "rank0_whole_block_bytes_per_step": xst[2] / args.steps}
         if kern:
             per = {}
             for name, (nl, tms, byt) in kern.items():

@@ -76,6 +76,15 @@ int misort_get_unique_id(void* id /* MISORT_UNIQUE_ID_BYTES */);
 /* Collective over all nranks processes: ncclCommInitRank. nranks must be a
  * power of two (else MISORT_E_NOT_POW2, the reference's abort condition). */
 int misort_comm_init(misort_ctx* ctx, int nranks, int rank, const void* id);
+/* In-process rank group: P ranks as P threads of one process, each with its own
+ * context (on the same or different GPUs).  The exchange is a device-to-device
+ * copy ordered by HIP events; the schedule, sizes and merge-split path are the
+ * same as over RCCL.  Used to run the P-rank path on one GPU (tests) and to
+ * drive several GPUs from one process. */
+typedef struct misort_group misort_group;
+int misort_group_create(int nranks, misort_group** out);
+int misort_group_destroy(misort_group* g);
+int misort_comm_init_group(misort_ctx* ctx, misort_group* g, int rank);
 int misort_comm_size(misort_ctx* ctx);  /* numprocs */
 int misort_comm_rank(misort_ctx* ctx);  /* myid */
 /* psort.cc:182-196 stage schedule of `rank` in a `p`-rank hypercube: partner
@@ -99,7 +108,16 @@ int64_t misort_block_size(int64_t n, int p, int rank);
 int misort_parallel_bitonic_sort(misort_ctx* ctx, int dtype, void* d_keys, int64_t loc_size,
                                  int64_t max_size, void* stream);
 /* Same, out of place: d_in is left unchanged, d_out receives the block
- * (d_in == d_out allowed). */
+ * (d_in == d_out allowed).
+ *
+ * Exchange volume: before each compare-split the partners swap splitter
+ * samples (every S-th key, S = max(256, n/32768)) and both derive the same
+ * lower bound of the merge-path crossing point, so each side sends only the
+ * keys that can cross (the min side its top k, the max side its bottom k)
+ * instead of the whole block.  The kept multisets -- hence the bytes of the
+ * result -- are exactly those of the reference's whole-block MPI_Sendrecv.
+ * MISORT_FULL_EXCHANGE=1 (or misort_set_full_exchange) restores whole-block
+ * exchange. */
 int misort_parallel_bitonic_sort_oop(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
                                      int64_t loc_size, int64_t max_size, void* stream);
 
@@ -132,6 +150,11 @@ int misort_sort_host(misort_ctx* ctx, int dtype, const void* h_in, void* h_out, 
  * key_g = mix(seed + (g+1)*0x9E3779B97F4A7C15), u32 = top 32 bits. */
 int misort_fill_splitmix(misort_ctx* ctx, int dtype, void* d_out, int64_t n, uint64_t seed,
                          int64_t g0, void* stream);
+
+int misort_set_full_exchange(misort_ctx* ctx, int on);
+/* Exchange volume since the last call (then reset): compare-split stages,
+ * bytes sent+received, and the bytes a whole-block exchange would have moved. */
+int misort_exchange_stats(misort_ctx* ctx, int64_t* stages, int64_t* bytes, int64_t* full_bytes);
 
 /* ---- per-launch profiling (HIP events around every kernel launch) ---------- */
 int misort_profile_enable(misort_ctx* ctx, int on);

@@ -45,6 +45,11 @@ hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
 template <typename T>
 hipError_t count_descents(const T* a, int64_t n, unsigned long long* count, hipStream_t s);
 
+// out[c] = a[min(c*stride, n-1)] for c in [0, count): the splitter samples of a
+// sorted block used to bracket the compare-split crossing point.
+template <typename K>
+hipError_t gather_samples(const K* a, int64_t n, int64_t stride, K* out, int64_t count, hipStream_t s);
+
 // IEEE double bits <-> order-preserving u64, in place.
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s);
 hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s);

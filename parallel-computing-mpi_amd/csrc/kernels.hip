@@ -533,6 +533,15 @@ __global__ void k_count_desc(const T* __restrict__ a, int64_t n, unsigned long l
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
+template <typename K>
+__global__ void k_gather_samples(const K* __restrict__ a, int64_t n, int64_t stride, K* __restrict__ out,
+                                 int64_t count) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= count) return;
+    const int64_t x = c * stride < n - 1 ? c * stride : n - 1;
+    out[c] = a[x];
+}
+
 __global__ void k_f64_ord(uint64_t* a, int64_t n, int to_ord) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -744,6 +753,15 @@ hipError_t count_descents(const T* a, int64_t n, unsigned long long* count, hipS
     k_count_desc<T><<<stream_grid(n, 256), 256, 0, s>>>(a, n, count);
     return hipGetLastError();
 }
+
+template <typename K>
+hipError_t gather_samples(const K* a, int64_t n, int64_t stride, K* out, int64_t count, hipStream_t s) {
+    if (n <= 0 || count <= 0) return hipSuccess;
+    k_gather_samples<K><<<(unsigned)((count + 255) / 256), 256, 0, s>>>(a, n, stride, out, count);
+    return hipGetLastError();
+}
+template hipError_t gather_samples<uint32_t>(const uint32_t*, int64_t, int64_t, uint32_t*, int64_t, hipStream_t);
+template hipError_t gather_samples<uint64_t>(const uint64_t*, int64_t, int64_t, uint64_t*, int64_t, hipStream_t);
 
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;

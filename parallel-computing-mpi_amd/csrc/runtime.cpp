@@ -11,6 +11,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -136,17 +140,169 @@ struct DevBuf {
     }
 };
 
+// ---------------------------------------------------------------- transport
+//
+// The exchange step of compare_split (MPI_Sendrecv, psort.cc:121,146) and the
+// two small all-gathers the driver needs, behind one interface:
+//   RcclTransport   one process per GPU, ncclSend/ncclRecv over xGMI;
+//   LocalTransport  ranks are threads of one process (misort_group), the
+//                   exchange is a device-to-device copy ordered by HIP events.
+struct Transport {
+    int nranks = 1, rank = 0;
+    virtual ~Transport() = default;
+    // all ranks' int64 value, host-visible on return
+    virtual int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all,
+                              hipStream_t s) = 0;
+    // device buffers; both sides know both byte counts
+    virtual int sendrecv(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, int peer,
+                         hipStream_t s) = 0;
+};
+
+struct RcclTransport final : Transport {
+    ncclComm_t comm = nullptr;
+    DevBuf buf;
+    ~RcclTransport() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
+        int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
+        if (rc) return rc;
+        int64_t* d = (int64_t*)buf.p;
+        HIPCHK(hipMemcpyAsync(d + (size_t)count * nranks, mine, sizeof(int64_t) * count,
+                              hipMemcpyHostToDevice, s));
+        NCCLCHK(ncclAllGather(d + (size_t)count * nranks, d, count, ncclInt64, comm, s));
+        all.resize((size_t)count * nranks);
+        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return MISORT_OK;
+    }
+    int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
+        NCCLCHK(ncclGroupStart());
+        if (sb) NCCLCHK(ncclSend(send, sb, ncclUint8, peer, comm, s));
+        if (rb) NCCLCHK(ncclRecv(recv, rb, ncclUint8, peer, comm, s));
+        NCCLCHK(ncclGroupEnd());
+        return MISORT_OK;
+    }
+};
+
+}  // namespace
+
+// In-process rank group: one thread (and one misort_ctx) per rank.
+struct misort_group {
+    int n;
+    std::mutex mu;
+    std::condition_variable cv;
+    // Exchanges are matched per partner pair: posted[q]/finished[q] count this
+    // rank's exchanges with rank q, which both sides advance in the same order
+    // (a stage that moves nothing skips on both sides).
+    struct Slot {
+        const void* ptr = nullptr;
+        size_t bytes = 0;
+        hipEvent_t ready = nullptr, done = nullptr;
+        std::vector<uint64_t> posted, finished;
+        std::vector<int64_t> vals;
+    };
+    std::vector<Slot> slots;
+    uint64_t bar_count = 0, bar_gen = 0;
+    explicit misort_group(int n_) : n(n_), slots(n_) {
+        for (auto& sl : slots) {
+            sl.posted.assign(n_, 0);
+            sl.finished.assign(n_, 0);
+        }
+    }
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = bar_gen;
+        if (++bar_count == (uint64_t)n) {
+            bar_count = 0;
+            ++bar_gen;
+            cv.notify_all();
+            return true;
+        }
+        return cv.wait_for(lk, std::chrono::seconds(120), [&] { return bar_gen != gen; });
+    }
+};
+
+namespace {
+
+struct LocalTransport final : Transport {
+    misort_group* g = nullptr;
+    std::vector<uint64_t> epoch;  // exchanges with each peer so far
+    ~LocalTransport() override {
+        auto& me = g->slots[rank];
+        if (me.ready) (void)hipEventDestroy(me.ready);
+        if (me.done) (void)hipEventDestroy(me.done);
+        me.ready = me.done = nullptr;
+    }
+    int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t) override {
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            g->slots[rank].vals.assign(mine, mine + count);
+        }
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        all.clear();
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            for (int r = 0; r < nranks; ++r)
+                all.insert(all.end(), g->slots[r].vals.begin(), g->slots[r].vals.end());
+        }
+        if (!g->barrier())  // nobody overwrites vals before everyone has read them
+            return fail(MISORT_E_INVALID, "group barrier timed out");
+        return MISORT_OK;
+    }
+    int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
+        auto& me = g->slots[rank];
+        auto& pe = g->slots[peer];
+        const uint64_t e = ++epoch[peer];
+        HIPCHK(hipEventRecord(me.ready, s));
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            me.ptr = send;
+            me.bytes = sb;
+            me.posted[peer] = e;
+        }
+        g->cv.notify_all();
+        {
+            std::unique_lock<std::mutex> lk(g->mu);
+            if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return pe.posted[rank] >= e; }))
+                return fail(MISORT_E_INVALID, "group exchange %d<->%d timed out", rank, peer);
+        }
+        if (pe.bytes != rb)
+            return fail(MISORT_E_INVALID, "sendrecv size mismatch with rank %d (%zu vs %zu)", peer,
+                        pe.bytes, rb);
+        HIPCHK(hipStreamWaitEvent(s, pe.ready, 0));
+        if (rb) HIPCHK(hipMemcpyAsync(recv, pe.ptr, rb, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipEventRecord(me.done, s));
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            me.finished[peer] = e;
+        }
+        g->cv.notify_all();
+        {
+            std::unique_lock<std::mutex> lk(g->mu);
+            if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return pe.finished[rank] >= e; }))
+                return fail(MISORT_E_INVALID, "group exchange %d<->%d timed out", rank, peer);
+        }
+        // the peer has read my send buffer before this stream reuses it
+        HIPCHK(hipStreamWaitEvent(s, pe.done, 0));
+        return MISORT_OK;
+    }
+};
+
 }  // namespace
 
 struct misort_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
+    Transport* tr = nullptr;
     int nranks = 1, rank = 0;
-    DevBuf work, recv, scratch, small;
+    DevBuf work, recv, scratch, small, samp_me, samp_peer;
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     Profiler prof;
+    int64_t xchg_bytes = 0, xchg_stages = 0, xchg_full_bytes = 0;
+    bool full_exchange = getenv("MISORT_FULL_EXCHANGE") != nullptr;
+    ~misort_ctx() { delete tr; }
 };
 
 namespace {
@@ -181,22 +337,30 @@ int do_merge_split(misort_ctx* c, int dtype, const void* a, int64_t na, const vo
     return MISORT_OK;
 }
 
-// Block sizes of every rank (the reference learns the partner's size from
-// MPI_Get_count, psort.cc:125,150; one all-gather up front gives all of them).
-int gather_sizes(misort_ctx* c, int64_t loc, std::vector<int64_t>& sizes, hipStream_t s) {
-    sizes.assign(c->nranks, 0);
-    if (c->nranks == 1) {
-        sizes[0] = loc;
-        return MISORT_OK;
+// Splitter samples of a sorted block: a[min(c*S, n-1)], c = 0..ceil(n/S).
+int64_t sample_stride(int64_t n) { return std::max<int64_t>(256, (n + 32767) / 32768); }
+int64_t sample_count(int64_t n) { return n <= 0 ? 0 : (n + sample_stride(n) - 1) / sample_stride(n) + 1; }
+
+// Lower bound of the merge-path co-rank i* = #A keys among the n_a smallest
+// of A U B (A first on ties), from the two sample sets alone.  For i < i_lo
+// A[i] <= B[n_a-1-i] is certain, so i* >= i_lo.  Both partners evaluate this
+// on the same samples, so they agree on the exchange size without another
+// round trip.
+template <typename T>
+int64_t corank_lower(const std::vector<T>& sa, int64_t na, const std::vector<T>& sb, int64_t nb) {
+    if (na == 0) return 0;
+    if (nb == 0) return na;
+    const int64_t Sa = sample_stride(na), Sb = sample_stride(nb);
+    const int64_t Ca = (int64_t)sa.size() - 1, Cb = (int64_t)sb.size() - 1;
+    auto upperA = [&](int64_t i) { return sa[std::min(i / Sa + 1, Ca)]; };
+    auto lowerB = [&](int64_t j) { return sb[std::min(j / Sb, Cb)]; };
+    int64_t lo = na > nb ? na - nb : 0, hi = na;  // answer in [lo, hi]
+    while (lo < hi) {  // first i whose "A[i] <= B[na-1-i]" is not certain
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (upperA(mid) <= lowerB(na - 1 - mid)) lo = mid + 1;
+        else hi = mid;
     }
-    int rc = c->small.ensure(sizeof(int64_t) * (c->nranks + 1));
-    if (rc) return rc;
-    int64_t* d = (int64_t*)c->small.p;
-    HIPCHK(hipMemcpyAsync(d + c->nranks, &loc, sizeof(int64_t), hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclAllGather(d + c->nranks, d, 1, ncclInt64, c->comm, s));
-    HIPCHK(hipMemcpyAsync(sizes.data(), d, sizeof(int64_t) * c->nranks, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    return MISORT_OK;
+    return lo;
 }
 
 int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
@@ -206,9 +370,9 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                                                (long long)loc, (long long)max_size);
     const int p = c->nranks;
     if (p & (p - 1)) return fail(MISORT_E_NOT_POW2, "bitonic sort requires 2^d processors");
-    std::vector<int64_t> sizes;
-    int rc = gather_sizes(c, loc, sizes, s);
-    if (rc) return rc;
+    int rc;
+    std::vector<int64_t> sizes(1, loc);
+    if (p > 1 && (rc = c->tr->allgather_i64(&loc, 1, sizes, s))) return rc;
     for (int r = 0; r < p; ++r)
         if (sizes[r] > max_size)
             return fail(MISORT_E_CAPACITY, "rank %d holds %lld keys > max_size %lld", r,
@@ -219,26 +383,78 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     const bool f64 = dtype == MISORT_F64;
     void* work = nullptr;
     if (nst > 0) {
-        int64_t maxp = 0;
-        for (int st = 0; st < nst; ++st) maxp = std::max(maxp, sizes[partner[st]]);
-        if ((rc = c->work.ensure(std::max<size_t>(1, (size_t)loc * w)))) return rc;
-        if ((rc = c->recv.ensure(std::max<size_t>(1, (size_t)maxp * w)))) return rc;
+        int64_t maxp = 0, maxs = 0;
+        for (int st = 0; st < nst; ++st) {
+            maxp = std::max(maxp, sizes[partner[st]]);
+            maxs = std::max(maxs, sample_count(sizes[partner[st]]));
+        }
+        if ((rc = c->work.ensure(std::max<size_t>(16, (size_t)loc * w)))) return rc;
+        if ((rc = c->recv.ensure(std::max<size_t>(16, (size_t)maxp * w)))) return rc;
+        if ((rc = c->samp_me.ensure(std::max<size_t>(16, (size_t)sample_count(loc) * w)))) return rc;
+        if ((rc = c->samp_peer.ensure(std::max<size_t>(16, (size_t)maxs * w)))) return rc;
         work = c->work.p;
     }
     // The local sort writes where the stage parity leaves the result in `out`.
     void* cur = (nst & 1) ? work : out;
     if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s))) return rc;
     void* other = (cur == work) ? out : work;
-    const ncclDataType_t nt = w == 4 ? ncclUint32 : ncclUint64;
     for (int st = 0; st < nst; ++st) {
         const int q = partner[st];
-        NCCLCHK(ncclGroupStart());
-        NCCLCHK(ncclSend(cur, (size_t)loc, nt, q, c->comm, s));
-        NCCLCHK(ncclRecv(c->recv.p, (size_t)sizes[q], nt, q, c->comm, s));
-        NCCLCHK(ncclGroupEnd());
-        if ((rc = do_merge_split(c, dtype, cur, loc, c->recv.p, sizes[q], other, keep[st], s))) return rc;
+        const int64_t nq = sizes[q];
+        const bool mx = keep[st] != 0;  // this rank keeps the upper part
+        // min side = "A" (keeps its n_a smallest), max side = "B"
+        const int64_t na = mx ? nq : loc, nb = mx ? loc : nq;
+        int64_t k;  // keys each side sends: A's top k, B's bottom k
+        if (c->full_exchange || loc == 0 || nq == 0) {
+            k = -1;
+        } else {
+            const int64_t cm = sample_count(loc), cq = sample_count(nq);
+            hipError_t e = w == 4 ? misort::gather_samples<uint32_t>((const uint32_t*)cur, loc, sample_stride(loc),
+                                                                     (uint32_t*)c->samp_me.p, cm, s)
+                                  : misort::gather_samples<uint64_t>((const uint64_t*)cur, loc, sample_stride(loc),
+                                                                     (uint64_t*)c->samp_me.p, cm, s);
+            if (e != hipSuccess) return fail(MISORT_E_HIP, "gather_samples: %s", hipGetErrorString(e));
+            if ((rc = c->tr->sendrecv(c->samp_me.p, (size_t)cm * w, c->samp_peer.p, (size_t)cq * w, q, s)))
+                return rc;
+            int64_t ilo;
+            if (w == 4) {
+                std::vector<uint32_t> me(cm), pe(cq);
+                HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
+            } else {
+                std::vector<uint64_t> me(cm), pe(cq);
+                HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
+            }
+            k = na - ilo;
+        }
+        c->xchg_stages += 1;
+        c->xchg_full_bytes += (int64_t)((loc + nq) * w);
+        if (k == 0) continue;  // no key crosses: both blocks stay as they are
+        // A sends its top k = A[na-k, na); B sends its bottom k = B[0, k)
+        const void* sbuf;
+        size_t sbytes, rbytes;
+        int64_t nrecv;
+        if (k < 0) {  // whole blocks, as MPI_Sendrecv does
+            sbuf = cur;
+            sbytes = (size_t)loc * w;
+            rbytes = (size_t)nq * w;
+            nrecv = nq;
+        } else {
+            sbuf = mx ? cur : (const char*)cur + (size_t)(loc - k) * w;
+            sbytes = rbytes = (size_t)k * w;
+            nrecv = k;
+        }
+        if ((rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s))) return rc;
+        c->xchg_bytes += (int64_t)(sbytes + rbytes);
+        if ((rc = do_merge_split(c, dtype, cur, loc, c->recv.p, nrecv, other, keep[st], s))) return rc;
         std::swap(cur, other);
     }
+    if (cur != out && loc > 0) HIPCHK(hipMemcpyAsync(out, cur, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
     if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, loc, s));
     return MISORT_OK;
 }
@@ -271,7 +487,8 @@ int misort_destroy(misort_ctx* c) {
     if (!c) return MISORT_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm) ncclCommDestroy(c->comm);
+    delete c->tr;
+    c->tr = nullptr;
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -300,17 +517,76 @@ int misort_comm_init(misort_ctx* c, int nranks, int rank, const void* id) {
         return fail(MISORT_E_INVALID, "bad communicator arguments");
     if (nranks & (nranks - 1)) return fail(MISORT_E_NOT_POW2, "bitonic sort requires 2^d processors");
     HIPCHK(hipSetDevice(c->device));
-    if (c->comm) {
-        ncclCommDestroy(c->comm);
-        c->comm = nullptr;
-    }
+    delete c->tr;
+    c->tr = nullptr;
+    c->nranks = 1;
+    c->rank = 0;
     if (nranks > 1) {
+        auto* t = new RcclTransport();
         ncclUniqueId u;
         memcpy(&u, id, sizeof u);
-        NCCLCHK(ncclCommInitRank(&c->comm, nranks, u, rank));
+        ncclResult_t r = ncclCommInitRank(&t->comm, nranks, u, rank);
+        if (r != ncclSuccess) {
+            delete t;
+            return fail(MISORT_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+        t->nranks = nranks;
+        t->rank = rank;
+        c->tr = t;
     }
     c->nranks = nranks;
     c->rank = rank;
+    return MISORT_OK;
+}
+
+int misort_group_create(int nranks, misort_group** out) try {
+    if (!out || nranks < 1) return fail(MISORT_E_INVALID, "bad group arguments");
+    if (nranks & (nranks - 1)) return fail(MISORT_E_NOT_POW2, "bitonic sort requires 2^d processors");
+    *out = new misort_group(nranks);
+    return MISORT_OK;
+} catch (const std::bad_alloc&) {
+    return fail(MISORT_E_INVALID, "out of host memory");
+}
+
+int misort_group_destroy(misort_group* g) {
+    delete g;
+    return MISORT_OK;
+}
+
+int misort_comm_init_group(misort_ctx* c, misort_group* g, int rank) {
+    if (!c || !g || rank < 0 || rank >= g->n) return fail(MISORT_E_INVALID, "bad group rank");
+    HIPCHK(hipSetDevice(c->device));
+    delete c->tr;
+    c->tr = nullptr;
+    auto* t = new LocalTransport();
+    t->g = g;
+    t->nranks = g->n;
+    t->rank = rank;
+    t->epoch.assign(g->n, 0);
+    auto& slot = g->slots[rank];
+    if (hipEventCreateWithFlags(&slot.ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&slot.done, hipEventDisableTiming) != hipSuccess) {
+        delete t;
+        return fail(MISORT_E_HIP, "hipEventCreate failed");
+    }
+    c->tr = t;
+    c->nranks = g->n;
+    c->rank = rank;
+    return MISORT_OK;
+}
+
+int misort_set_full_exchange(misort_ctx* c, int on) {
+    if (!c) return fail(MISORT_E_INVALID, "null ctx");
+    c->full_exchange = on != 0;
+    return MISORT_OK;
+}
+
+int misort_exchange_stats(misort_ctx* c, int64_t* stages, int64_t* bytes, int64_t* full_bytes) {
+    if (!c) return fail(MISORT_E_INVALID, "null ctx");
+    if (stages) *stages = c->xchg_stages;
+    if (bytes) *bytes = c->xchg_bytes;
+    if (full_bytes) *full_bytes = c->xchg_full_bytes;
+    c->xchg_stages = c->xchg_bytes = c->xchg_full_bytes = 0;
     return MISORT_OK;
 }
 
@@ -352,7 +628,7 @@ int misort_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64
 int misort_parallel_bitonic_sort_oop(misort_ctx* c, int dtype, const void* in, void* out,
                                      int64_t loc, int64_t max_size, void* stream) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
-    if (c->nranks > 1 && !c->comm) return fail(MISORT_E_NO_COMM, "communicator not initialised");
+    if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     if (loc > 0 && (!in || !out)) return fail(MISORT_E_INVALID, "null buffer");
     return parallel_sort(c, dtype, in, out, loc, max_size, pick(c, stream));
 }
@@ -385,14 +661,13 @@ int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc
 int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int64_t* errors,
                       void* stream) {
     if (!c || !valid_dtype(dtype) || n < 0 || !errors) return fail(MISORT_E_INVALID, "bad check args");
-    if (c->nranks > 1 && !c->comm) return fail(MISORT_E_NO_COMM, "communicator not initialised");
+    if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     hipStream_t s = pick(c, stream);
     const int p = c->nranks;
     // Per rank: {local descents, n, first key bits, last key bits}.
-    int rc = c->small.ensure(sizeof(uint64_t) * 4 * (p + 1) + 64);
+    int rc = c->small.ensure(sizeof(uint64_t) * 4 + 64);
     if (rc) return rc;
-    uint64_t* d = (uint64_t*)c->small.p;
-    uint64_t* mine = d + 4 * p;
+    uint64_t* mine = (uint64_t*)c->small.p;
     HIPCHK(hipMemsetAsync(mine, 0, sizeof(uint64_t) * 4, s));
     hipError_t e = hipSuccess;
     if (dtype == MISORT_U32) e = misort::count_descents<uint32_t>((const uint32_t*)keys, n, (unsigned long long*)mine, s);
@@ -406,14 +681,12 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
         HIPCHK(hipMemcpyAsync(mine + 2, keys, w, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(mine + 3, (const char*)keys + (size_t)(n - 1) * w, w, hipMemcpyDeviceToDevice, s));
     }
-    std::vector<uint64_t> all(4 * (size_t)p);
-    if (p > 1) {
-        NCCLCHK(ncclAllGather(mine, d, 4, ncclUint64, c->comm, s));
-        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(uint64_t) * 4 * p, hipMemcpyDeviceToHost, s));
-    } else {
-        HIPCHK(hipMemcpyAsync(all.data(), mine, sizeof(uint64_t) * 4, hipMemcpyDeviceToHost, s));
-    }
+    int64_t four[4];
+    HIPCHK(hipMemcpyAsync(four, mine, sizeof four, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    std::vector<int64_t> alli(four, four + 4);
+    if (p > 1 && (rc = c->tr->allgather_i64(four, 4, alli, s))) return rc;
+    std::vector<uint64_t> all(alli.begin(), alli.end());
     // psort.cc:498-516: local descents + (rank>0) last(rank-1) > first(rank), SUM.
     int64_t total = 0;
     bool have_prev = false;

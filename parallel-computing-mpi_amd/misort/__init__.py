@@ -18,7 +18,7 @@ import os
 
 __all__ = [
     "U32", "U64", "F64", "MisortError", "NotPowerOfTwo", "NativeLibraryMissing",
-    "library_path", "lib", "Context", "block_sizes", "schedule", "tile_log2",
+    "library_path", "lib", "Context", "Group", "block_sizes", "schedule", "tile_log2",
 ]
 
 U32, U64, F64 = 0, 1, 2
@@ -83,6 +83,12 @@ def lib():
         "misort_profile_read": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_tile_log2": ([i32], i32),
+        "misort_group_create": ([i32, ctypes.POINTER(vp)], i32),
+        "misort_group_destroy": ([vp], i32),
+        "misort_comm_init_group": ([vp, vp, i32], i32),
+        "misort_set_full_exchange": ([vp, i32], i32),
+        "misort_exchange_stats": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                   ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -116,6 +122,48 @@ def schedule(p, rank):
 
 def tile_log2(key_bytes):
     return int(lib().misort_tile_log2(key_bytes))
+
+
+class Group:
+    """In-process rank group: P ranks = P threads, one Context each (the
+    exchange is a device-to-device copy; same schedule and merge-split as RCCL)."""
+
+    def __init__(self, nranks):
+        self._h = ctypes.c_void_p()
+        _check(lib().misort_group_create(nranks, ctypes.byref(self._h)))
+        self.nranks = nranks
+
+    def close(self):
+        if self._h:
+            lib().misort_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def run(self, fn, devices=None):
+        """Run fn(rank, ctx) on one thread per rank; returns the results."""
+        import threading
+        res, err = [None] * self.nranks, []
+        ctxs = [Context((devices or [0])[r % len(devices or [0])]) for r in range(self.nranks)]
+        for r, c in enumerate(ctxs):
+            _check(lib().misort_comm_init_group(c._h, self._h, r))
+
+        def body(r):
+            try:
+                import torch
+                torch.cuda.set_device(ctxs[r].device)
+                res[r] = fn(r, ctxs[r])
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                err.append(e)
+
+        th = [threading.Thread(target=body, args=(r,)) for r in range(self.nranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for c in ctxs:
+            c.close()
+        if err:
+            raise err[0]
+        return res
 
 
 def _dtype_of(t):
@@ -251,6 +299,20 @@ class Context:
 
     def synchronize(self):
         _check(lib().misort_synchronize(self._h))
+
+    @property
+    def native_stream(self):
+        """The context's own hipStream_t (int), for stream=..."""
+        return int(lib().misort_stream(self._h) or 0)
+
+    def set_full_exchange(self, on=True):
+        _check(lib().misort_set_full_exchange(self._h, int(on)))
+
+    def exchange_stats(self):
+        """(stages, bytes moved, bytes a whole-block exchange would move); resets."""
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _check(lib().misort_exchange_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return int(a.value), int(b.value), int(c.value)
 
     # ---- profiling ----------------------------------------------------------------
     def profile(self, on=True):
