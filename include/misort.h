@@ -152,6 +152,17 @@ int misort_fill_splitmix(misort_ctx* ctx, int dtype, void* d_out, int64_t n, uin
                          int64_t g0, void* stream);
 
 int misort_set_full_exchange(misort_ctx* ctx, int on);
+/* Host logic of the bracketed exchange (pure functions, no GPU):
+ * samples of a sorted block of n keys are keys[min(c*S, n-1)], c = 0..count-1,
+ * S = misort_sample_stride(n), count = misort_sample_count(n).
+ * misort_exchange_count returns k, the keys each partner sends (the keep-min
+ * side its top k, the keep-max side its bottom k), given both sample sets; -1
+ * means whole blocks (an empty side).  u64/f64 samples are order-preserving
+ * u64 patterns. */
+int64_t misort_sample_stride(int64_t n);
+int64_t misort_sample_count(int64_t n);
+int64_t misort_exchange_count(int dtype, const void* samples_min, int64_t n_min,
+                              const void* samples_max, int64_t n_max);
 /* Exchange volume since the last call (then reset): compare-split stages,
  * bytes sent+received, and the bytes a whole-block exchange would have moved. */
 int misort_exchange_stats(misort_ctx* ctx, int64_t* stages, int64_t* bytes, int64_t* full_bytes);

@@ -631,7 +631,9 @@ namespace {
 // the register-only pass instead (default 0 = never).
 struct PlanKnobs {
     int rmax = RMAX_ROWS, regpass = 0;
+    int grid_mult = 1;  // MISORT_GRID_MULT: persistent grid = mult x resident capacity (0 = one tile per workgroup)
     PlanKnobs() {
+        if (const char* e = getenv("MISORT_GRID_MULT")) grid_mult = atoi(e) < 0 ? 0 : atoi(e);
         if (const char* e = getenv("MISORT_RMAX")) rmax = atoi(e) < 1 ? 1 : atoi(e);
         if (rmax > RMAX_ROWS) rmax = RMAX_ROWS;
         if (const char* e = getenv("MISORT_REGPASS")) regpass = atoi(e);
@@ -655,7 +657,9 @@ void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t
                                                            G::NT, 0);
         cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
     }
-    const int64_t grid = m.ntiles < cap ? m.ntiles : cap;
+    const int gm = knobs().grid_mult;
+    const int64_t want = gm == 0 ? m.ntiles : cap * gm;
+    const int64_t grid = m.ntiles < want ? m.ntiles : want;
     if (grid > 0) k_stream<K, LT, MODE, R, FLIP, ORD><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
 }
 

@@ -575,6 +575,28 @@ int misort_comm_init_group(misort_ctx* c, misort_group* g, int rank) {
     return MISORT_OK;
 }
 
+int64_t misort_sample_stride(int64_t n) { return n < 0 ? MISORT_E_INVALID : sample_stride(n); }
+int64_t misort_sample_count(int64_t n) { return n < 0 ? MISORT_E_INVALID : sample_count(n); }
+
+int64_t misort_exchange_count(int dtype, const void* samples_min, int64_t n_min, const void* samples_max,
+                              int64_t n_max) {
+    if (!valid_dtype(dtype) || n_min < 0 || n_max < 0) return fail(MISORT_E_INVALID, "bad exchange args");
+    if (n_min == 0 || n_max == 0) return -1;  // whole (possibly empty) blocks
+    const int64_t ca = sample_count(n_min), cb = sample_count(n_max);
+    int64_t ilo;
+    if (dtype == MISORT_U32) {
+        std::vector<uint32_t> a((const uint32_t*)samples_min, (const uint32_t*)samples_min + ca);
+        std::vector<uint32_t> b((const uint32_t*)samples_max, (const uint32_t*)samples_max + cb);
+        ilo = corank_lower(a, n_min, b, n_max);
+    } else {
+        // u64 keys, or f64 keys already mapped to order-preserving u64
+        std::vector<uint64_t> a((const uint64_t*)samples_min, (const uint64_t*)samples_min + ca);
+        std::vector<uint64_t> b((const uint64_t*)samples_max, (const uint64_t*)samples_max + cb);
+        ilo = corank_lower(a, n_min, b, n_max);
+    }
+    return n_min - ilo;
+}
+
 int misort_set_full_exchange(misort_ctx* c, int on) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
     c->full_exchange = on != 0;

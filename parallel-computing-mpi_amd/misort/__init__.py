@@ -19,6 +19,7 @@ import os
 __all__ = [
     "U32", "U64", "F64", "MisortError", "NotPowerOfTwo", "NativeLibraryMissing",
     "library_path", "lib", "Context", "Group", "block_sizes", "schedule", "tile_log2",
+    "sample_indices", "exchange_count",
 ]
 
 U32, U64, F64 = 0, 1, 2
@@ -87,6 +88,9 @@ def lib():
         "misort_group_destroy": ([vp], i32),
         "misort_comm_init_group": ([vp, vp, i32], i32),
         "misort_set_full_exchange": ([vp, i32], i32),
+        "misort_sample_stride": ([i64], i64),
+        "misort_sample_count": ([i64], i64),
+        "misort_exchange_count": ([i32, vp, i64, vp, i64], i64),
         "misort_exchange_stats": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                    ctypes.POINTER(i64)], i32),
     }
@@ -118,6 +122,24 @@ def schedule(p, rank):
     keep = (ctypes.c_int * 64)()
     s = _check(lib().misort_bitonic_schedule(p, rank, partner, keep))
     return [(partner[i], keep[i]) for i in range(s)]
+
+
+def sample_indices(n):
+    """Indices of the splitter samples of a sorted n-key block."""
+    import numpy as np
+    if n <= 0:
+        return np.zeros(0, dtype=np.int64)
+    S, C = int(lib().misort_sample_stride(n)), int(lib().misort_sample_count(n))
+    return np.minimum(np.arange(C, dtype=np.int64) * S, n - 1)
+
+
+def exchange_count(samples_min, n_min, samples_max, n_max):
+    """k keys each side sends in a compare-split (-1 = whole blocks)."""
+    import numpy as np
+    a, b = np.ascontiguousarray(samples_min), np.ascontiguousarray(samples_max)
+    dt = U32 if a.dtype == np.uint32 else U64
+    return int(lib().misort_exchange_count(dt, a.ctypes.data_as(ctypes.c_void_p), n_min,
+                                           b.ctypes.data_as(ctypes.c_void_p), n_max))
 
 
 def tile_log2(key_bytes):
