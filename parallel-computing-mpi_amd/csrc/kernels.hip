@@ -276,7 +276,9 @@ __device__ __forceinline__ void tile_fetch(K (*pre)[KT<K>::V], const K* src, con
         const int64_t gi = tile_index<LT, MODE>(m, tile, e);
         typename KT<K>::vec x;
         if (full) {
-            x = *reinterpret_cast<const typename KT<K>::vec*>(src + gi);
+            // streamed once per pass: non-temporal (measured +10 % on this shape,
+            // tools/hbm_shapes.hip)
+            x = __builtin_nontemporal_load(reinterpret_cast<const typename KT<K>::vec*>(src + gi));
             if constexpr (ORD) {
 #pragma unroll
                 for (int j = 0; j < G::V; ++j) x[j] = ord_of_f64(x[j]);
@@ -301,7 +303,7 @@ __device__ __forceinline__ void store_slot(K* dst, const TileMap& m, int64_t til
         typename KT<K>::vec x;
 #pragma unroll
         for (int j = 0; j < KT<K>::V; ++j) x[j] = w[j];
-        *reinterpret_cast<typename KT<K>::vec*>(dst + gi) = x;
+        __builtin_nontemporal_store(x, reinterpret_cast<typename KT<K>::vec*>(dst + gi));
     } else {
         store_vec<K>(dst, gi, n, w);
     }
@@ -631,7 +633,8 @@ namespace {
 // the register-only pass instead (default 0 = never).
 struct PlanKnobs {
     int rmax = RMAX_ROWS, regpass = 0;
-    int grid_mult = 1;  // MISORT_GRID_MULT: persistent grid = mult x resident capacity (0 = one tile per workgroup)
+    int grid_mult = 0;  // MISORT_GRID_MULT: persistent grid = mult x resident capacity; 0 (default) =
+                        // one tile per workgroup, measured faster than any persistent grid
     PlanKnobs() {
         if (const char* e = getenv("MISORT_GRID_MULT")) grid_mult = atoi(e) < 0 ? 0 : atoi(e);
         if (const char* e = getenv("MISORT_RMAX")) rmax = atoi(e) < 1 ? 1 : atoi(e);
