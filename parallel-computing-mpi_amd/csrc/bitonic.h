@@ -1,0 +1,551 @@
+// bitonic.h -- the gfx950 (CDNA4) bitonic tile engine and its pass planner.
+//
+// Replaces the reference's local std::sort (psort.cc:175).  Written for wave64 /
+// 160 KiB LDS / 8 TB/s HBM3E; no MFMA (sorting is not a contraction).  Included
+// by one translation unit per key type (sort_u32.hip, sort_u64.hip), which
+// instantiate local_sort<K>; kernels.hip uses only the shared device helpers.
+//
+// Sorting network: bitonic sort in the "flip" formulation.  Level m (blocks of
+// s = 2^m keys) starts with the flip stage, which compares i with its mirror
+// i ^ (s-1), and continues with half-cleaner stages i <-> i ^ 2^j for
+// j = m-2 .. 0.  Every compare-exchange puts the minimum at the lower index, so
+// no direction bits exist and every block is ascending after its level.  A
+// sentinel (all-ones) suffix can only move upwards, so the padding of n up to a
+// power of two is VIRTUAL: indices >= n read as all-ones and are never stored.
+//
+// Passes over HBM (each moves every key once in and once out):
+//   k_stream<SORT>   levels 1..LT of every 2^LT-key tile in LDS;
+//   k_stream<ROWS>   up to LT-5 consecutive large strides of one level: a tile
+//                    is 2^R rows at the stride distance times 2^(LT-R)
+//                    consecutive keys, so every row segment is a coalesced
+//                    >= 128 B run;
+//   k_stream<MERGE>  the strides < 2^LT of one level, in an LDS tile.
+// All of them share one tile engine (one-shot or persistent + prefetching).
+//
+// A pass over n keys moves 2 * n * sizeof(K) algorithmic HBM bytes.
+#pragma once
+#include <stdlib.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace misort {
+
+// Pass-planner knobs (environment, read once per process, kernels.hip):
+//   MISORT_TILE_LOG2       SORT/MERGE tile, log2 u32 keys: 15 (default: 128 KiB
+//                          of LDS, one 1024-lane workgroup per CU) or 14 (64 KiB,
+//                          two 512-lane workgroups per CU); u64 tiles are half;
+//   MISORT_ROWS_TILE_LOG2  the same for ROWS passes (default 15);
+//   MISORT_RMAX            most strides one ROWS pass fuses (cap LT_rows - 5);
+//   MISORT_PERSIST         tile modes (bit 1 << TileMode: 1 SORT, 2 MERGE, 4 ROWS)
+//                          that run a persistent grid of MISORT_GRID_MULT x the
+//                          resident capacity with the next tile's loads in
+//                          flight (default 3); the others launch one workgroup
+//                          per tile;
+//   MISORT_PINGPONG        1 (default): passes alternate between the output and
+//                          a scratch buffer (copy-shaped HBM traffic); 0: in place.
+struct PlanKnobs {
+    int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3, grid_mult = 1, pingpong = 1;
+    PlanKnobs();
+};
+const PlanKnobs& plan_knobs();
+
+namespace {
+
+template <typename K>
+struct KT;
+template <>
+struct KT<uint32_t> {
+    static constexpr uint32_t MAX = 0xFFFFFFFFu;
+    static constexpr int V = 4;         // keys per 16-byte vector
+    static constexpr int LT_SMALL = 14; // log2 keys per half-size LDS tile (64 KiB + padding)
+    typedef uint32_t vec __attribute__((ext_vector_type(4)));
+};
+template <>
+struct KT<uint64_t> {
+    static constexpr uint64_t MAX = ~0ull;
+    static constexpr int V = 2;
+    static constexpr int LT_SMALL = 13;
+    typedef uint64_t vec __attribute__((ext_vector_type(2)));
+};
+
+constexpr int RMAX_ROWS = 10;   // most strides one ROWS pass fuses (LT - R >= 5: 128-B row runs)
+
+__device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
+    return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+}
+
+template <typename K>
+__device__ __forceinline__ void cx(K& a, K& b) {
+    const K lo = __builtin_elementwise_min(a, b);
+    const K hi = __builtin_elementwise_max(a, b);
+    a = lo;
+    b = hi;
+}
+
+// 16-byte vector load of keys [i0, i0+V); indices >= n read as the sentinel.
+template <typename K, bool ORD>
+__device__ __forceinline__ void load_vec(const K* __restrict__ p, int64_t i0, int64_t n,
+                                         K (&w)[KT<K>::V]) {
+    constexpr int V = KT<K>::V;
+    if (i0 + V <= n) {
+        const typename KT<K>::vec x = *reinterpret_cast<const typename KT<K>::vec*>(p + i0);
+#pragma unroll
+        for (int j = 0; j < V; ++j) w[j] = x[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) w[j] = (i0 + j < n) ? p[i0 + j] : KT<K>::MAX;
+    }
+    if constexpr (ORD) {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+            if (i0 + j < n) w[j] = ord_of_f64(w[j]);
+    }
+}
+
+template <typename K>
+__device__ __forceinline__ void store_vec(K* __restrict__ p, int64_t i0, int64_t n,
+                                          const K (&w)[KT<K>::V]) {
+    constexpr int V = KT<K>::V;
+    if (i0 + V <= n) {
+        typename KT<K>::vec x;
+#pragma unroll
+        for (int j = 0; j < V; ++j) x[j] = w[j];
+        *reinterpret_cast<typename KT<K>::vec*>(p + i0) = x;
+    } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+            if (i0 + j < n) p[i0 + j] = w[j];
+    }
+}
+
+// ------------------------------------------------- streaming tile engine
+//
+// Persistent workgroups walk a list of 2^LT-key tiles.  While the LDS phases of
+// tile i run, the 16-byte loads of tile i+1 are already in flight into a
+// register buffer, so HBM streams continuously with 2 workgroups per CU.
+//
+// A tile is a set of 2^LT keys that one network segment touches only among
+// themselves, addressed through a "virtual" index v in [0, 2^LT):
+//   CONTIG   v -> tile*2^LT + v                       (tile sort / tile merge)
+//   ROWS     v = (c << logB) | j -> wbase + (c << lo) + low(c) + j
+//            2^R rows c at global stride 2^lo (the R strides 2^hi..2^lo of one
+//            level, R = LT - logB) times B = 2^logB consecutive keys.  For the
+//            first pass of a level (flip), rows whose top bit is set start at
+//            the mirrored block 2^lo - L0 - B, which turns the level's global
+//            flip i <-> i ^ (2^(hi+1) - 1) into the tile's own flip v <-> ~v.
+//
+// Register slots: lane t loads LOADS = 32/V vectors, slot k = virtual keys
+// (k*NT + t)*V .. +V-1, so the top KB = log2(LOADS) virtual bits are the slot
+// index and the bottom VB = log2(V) bits the vector component.  Strides on
+// those bits run in registers before the LDS write (slots) and after the LDS
+// read (components); only the strides in between cost an LDS phase.  For a
+// flip on the top slot bit the upper slots load the mirrored lane's vector
+// reversed, so every mirror pair meets in one lane at one component.
+//
+// LDS layout: key v at word v + v/32.  The padding keeps every phase's
+// 32-lane accesses on distinct banks, and since v + v/32 is additive over
+// disjoint bit fields every access is one base VGPR plus an immediate offset.
+enum TileMode : int { TM_SORT = 0, TM_MERGE = 1, TM_ROWS = 2 };
+
+struct TileMap {
+    int64_t ntiles;  // real tiles (a prefix of the tile list)
+    int lo, hi, logB, flip;
+};
+
+__host__ __device__ constexpr int pad(int v) { return v + (v >> 5); }
+
+template <typename K, int LT>
+struct TileGeo {
+    static constexpr int T = 1 << LT, NT = T / 32, V = KT<K>::V, LOADS = T / (NT * V);
+    static constexpr int KB = LOADS == 16 ? 4 : LOADS == 8 ? 3 : LOADS == 4 ? 2 : 1;
+    static constexpr int VB = V == 4 ? 2 : 1;
+    // LDS tile (keys + bank padding): 2 workgroups per CU up to 80 KiB, else 1
+    static constexpr int LDS = pad(T) * (int)sizeof(K);
+    static constexpr int WG_PER_CU = LDS <= 80 * 1024 ? 2 : 1;
+    static constexpr int WAVES_PER_EU = WG_PER_CU * NT / 256;  // -> VGPR budget per lane
+};
+
+template <int LT, int MODE>
+__device__ __forceinline__ int64_t tile_index(const TileMap& m, int64_t tile, int e) {
+    if constexpr (MODE != TM_ROWS) {
+        return (tile << LT) + e;
+    } else {
+        const int R = LT - m.logB;
+        const int sh = m.lo - m.logB;  // log2 tiles per 2^(hi+1) segment
+        const int64_t seg = tile >> sh, lb = tile & (((int64_t)1 << sh) - 1);
+        const int64_t L0 = lb << m.logB;
+        const int c = e >> m.logB, j = e & ((1 << m.logB) - 1);
+        const bool mir = m.flip && ((c >> (R - 1)) & 1);
+        const int64_t low = mir ? (((int64_t)1 << m.lo) - L0 - ((int64_t)1 << m.logB)) : L0;
+        return (seg << (m.hi + 1)) + ((int64_t)c << m.lo) + low + j;
+    }
+}
+
+// Every key of the tile lies below n (then no per-element bounds checks).
+template <int LT, int MODE>
+__device__ __forceinline__ bool tile_full(const TileMap& m, int64_t tile, int64_t n) {
+    if constexpr (MODE != TM_ROWS) {
+        return ((tile + 1) << LT) <= n;
+    } else {
+        return (((tile >> (m.lo - m.logB)) + 1) << (m.hi + 1)) <= n;
+    }
+}
+
+// Slot k of lane t: virtual vector start, and whether it is held mirrored.
+template <typename K, int LT, bool MIRROR>
+__device__ __forceinline__ int slot_lane(int k, int t) {
+    typedef TileGeo<K, LT> G;
+    return (MIRROR && k >= G::LOADS / 2) ? (G::NT - 1 - t) : t;
+}
+
+template <typename K, int LT, int MODE, bool MIRROR, bool ORD>
+__device__ __forceinline__ void tile_fetch(K (*pre)[KT<K>::V], const K* src, const TileMap& m,
+                                           int64_t tile, int64_t n, int t) {
+    typedef TileGeo<K, LT> G;
+    const bool full = tile_full<LT, MODE>(m, tile, n);
+#pragma unroll
+    for (int k = 0; k < G::LOADS; ++k) {
+        const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+        const int64_t gi = tile_index<LT, MODE>(m, tile, e);
+        typename KT<K>::vec x;
+        if (full) {
+            // streamed once per pass: non-temporal (measured +10 % on this shape,
+            // tools/hbm_shapes.hip)
+            x = __builtin_nontemporal_load(reinterpret_cast<const typename KT<K>::vec*>(src + gi));
+            if constexpr (ORD) {
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) x[j] = ord_of_f64(x[j]);
+            }
+        } else {
+            K w[G::V];
+            load_vec<K, ORD>(src, gi, n, w);
+#pragma unroll
+            for (int j = 0; j < G::V; ++j) x[j] = w[j];
+        }
+        const bool mk = MIRROR && k >= G::LOADS / 2;
+#pragma unroll
+        for (int j = 0; j < G::V; ++j) pre[k][j] = mk ? x[G::V - 1 - j] : x[j];
+    }
+}
+
+template <typename K, int LT, int MODE>
+__device__ __forceinline__ void store_slot(K* dst, const TileMap& m, int64_t tile, int64_t n,
+                                           bool full, int e, const K (&w)[KT<K>::V]) {
+    const int64_t gi = tile_index<LT, MODE>(m, tile, e);
+    if (full) {
+        typename KT<K>::vec x;
+#pragma unroll
+        for (int j = 0; j < KT<K>::V; ++j) x[j] = w[j];
+        __builtin_nontemporal_store(x, reinterpret_cast<typename KT<K>::vec*>(dst + gi));
+    } else {
+        store_vec<K>(dst, gi, n, w);
+    }
+}
+
+// Compile-time stage list on 32 register keys: relative bits TOP..TOP-CNT+1.
+template <typename K, int TOP, int CNT, bool FLIP>
+__device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
+#pragma unroll
+    for (int r = TOP; r > TOP - CNT; --r) {
+        const bool fl = FLIP && r == TOP;
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (!(c & (1 << r))) cx(v[c], v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))]);
+    }
+}
+
+// One LDS phase, window [B, B+5) of the virtual index, compile-time shape.
+template <typename K, int B, int TOP, int CNT, bool FLIP>
+__device__ __forceinline__ void phase_c(K* s, int t) {
+    constexpr int lowm = (1 << B) - 1;
+    const int tl = t & lowm;
+    const int th = (t >> B) << (B + 5);
+    const int a0 = pad(th | tl);
+    const int a1 = FLIP ? pad(th | (tl ^ lowm)) : a0;
+    K v[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) v[c] = s[(((c >> TOP) & 1) ? a1 : a0) + pad(c << B)];
+    reg_stages_c<K, TOP, CNT, FLIP>(v);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) s[(((c >> TOP) & 1) ? a1 : a0) + pad(c << B)] = v[c];
+}
+
+// Strides HI..STOP of the virtual index through LDS phases (flip first).
+template <typename K, int HI, int STOP, bool FLIP>
+__device__ __forceinline__ void lds_range(K* s, int t) {
+    if constexpr (HI >= STOP) {
+        constexpr int B = HI > 4 ? HI - 4 : 0;
+        constexpr int LOWEST = B > STOP ? B : STOP;
+        phase_c<K, B, HI - B, HI - LOWEST + 1, FLIP>(s, t);
+        __syncthreads();
+        lds_range<K, LOWEST - 1, STOP, false>(s, t);
+    }
+}
+
+// Levels L..LT of the tile sort (level 1..5 done by the caller).
+template <typename K, int L, int LT>
+__device__ __forceinline__ void sort_levels(K* s, int t) {
+    if constexpr (L <= LT) {
+        lds_range<K, L - 1, 0, true>(s, t);
+        sort_levels<K, L + 1, LT>(s, t);
+    }
+}
+
+// PERSIST: the grid is smaller than the tile list and every workgroup walks
+// tiles with the next tile's loads in flight; otherwise one tile per workgroup
+// (no prefetch registers live across the LDS phases).
+template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD, bool PERSIST>
+__global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_stream(
+    const K* in, K* out, int64_t n, TileMap m) {
+    typedef TileGeo<K, LT> G;
+    constexpr bool MIRROR = MODE == TM_ROWS && FLIP;
+    // slot-bit strides done in registers before the LDS write
+    constexpr int PRE = MODE == TM_MERGE ? G::KB : MODE == TM_ROWS ? (R < G::KB ? R : G::KB) : 0;
+    __shared__ K s[pad(G::T)];
+    const int t = threadIdx.x;
+    K pre[G::LOADS][G::V];
+    int64_t tile = blockIdx.x;
+    if (tile >= m.ntiles) return;
+    tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, tile, n, t);
+    for (; tile < m.ntiles; tile += gridDim.x) {
+#pragma unroll
+        for (int i = 0; i < PRE; ++i) {
+            const int r = G::KB - 1 - i;
+            const bool fl = MIRROR && i == 0;
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                if (k & (1 << r)) continue;
+                const int p = fl ? (k ^ (G::LOADS - 1)) : (k | (1 << r));
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) cx(pre[k][j], pre[p][j]);
+            }
+        }
+        const bool full = tile_full<LT, MODE>(m, tile, n);
+        if constexpr (MODE == TM_ROWS && R <= G::KB) {
+            // every stride of this pass was a slot bit: store straight from registers
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                K w[G::V];
+                const bool mk = MIRROR && k >= G::LOADS / 2;
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) w[j] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
+                store_slot<K, LT, MODE>(out, m, tile, n, full,
+                                        (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V, w);
+            }
+            const int64_t nxt = tile + gridDim.x;
+            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+        } else {
+            // registers -> LDS (mirrored slots to their own virtual position)
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                const bool mk = MIRROR && k >= G::LOADS / 2;
+                const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) s[pad(e + j)] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
+            }
+            __syncthreads();
+            const int64_t nxt = tile + gridDim.x;
+            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+            if constexpr (MODE == TM_SORT) {
+                {   // levels 1..5: window [0,5), 32 consecutive keys per lane
+                    K v[32];
+                    const int a0 = pad(t << 5);
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) v[c] = s[a0 + c];
+                    reg_stages_c<K, 0, 1, true>(v);
+                    reg_stages_c<K, 1, 2, true>(v);
+                    reg_stages_c<K, 2, 3, true>(v);
+                    reg_stages_c<K, 3, 4, true>(v);
+                    reg_stages_c<K, 4, 5, true>(v);
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) s[a0 + c] = v[c];
+                }
+                __syncthreads();
+                sort_levels<K, 6, LT>(s, t);
+            } else if constexpr (MODE == TM_MERGE) {
+                lds_range<K, LT - G::KB - 1, G::VB, false>(s, t);
+            } else {
+                lds_range<K, LT - G::KB - 1, LT - R, false>(s, t);
+            }
+            // LDS -> registers -> HBM; in a merge the vector-component strides run here
+#pragma unroll
+            for (int k = 0; k < G::LOADS; ++k) {
+                const int e = (k * G::NT + t) * G::V;
+                K w[G::V];
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) w[j] = s[pad(e + j)];
+                if constexpr (MODE == TM_MERGE) {
+#pragma unroll
+                    for (int r = G::VB - 1; r >= 0; --r)
+#pragma unroll
+                        for (int j = 0; j < G::V; ++j)
+                            if (!(j & (1 << r))) cx(w[j], w[j | (1 << r)]);
+                }
+                store_slot<K, LT, MODE>(out, m, tile, n, full, e, w);
+            }
+            __syncthreads();
+        }
+        if constexpr (!PERSIST) break;
+    }
+}
+
+
+[[maybe_unused]] int ceil_log2(int64_t n) {
+    int k = 0;
+    while (((int64_t)1 << k) < n) ++k;
+    return k;
+}
+
+struct HookScope {
+    LaunchHook* h;
+    Kind k;
+    hipStream_t s;
+    HookScope(LaunchHook* h_, Kind k_, double bytes, hipStream_t s_) : h(h_), k(k_), s(s_) {
+        if (h) h->before(k, bytes, s);
+    }
+    ~HookScope() {
+        if (h) h->after(k, s);
+    }
+};
+
+
+template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD>
+void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
+    typedef TileGeo<K, LT> G;
+    static int64_t cap = 0;  // resident workgroups for this instantiation
+    const bool persist = (plan_knobs().persist >> MODE) & 1;
+    if (persist && cap == 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_stream<K, LT, MODE, R, FLIP, ORD, true>,
+                                                           G::NT, 0);
+        cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
+    }
+    const int64_t want = persist ? cap * plan_knobs().grid_mult : m.ntiles;
+    const int64_t grid = m.ntiles < want ? m.ntiles : want;
+    if (grid <= 0) return;
+    if (persist) k_stream<K, LT, MODE, R, FLIP, ORD, true><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
+    else k_stream<K, LT, MODE, R, FLIP, ORD, false><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
+}
+
+template <typename K, int LT, int R>
+void launch_rows_r(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
+    if constexpr (R <= LT - 5) {
+        if (m.flip) launch_stream<K, LT, TM_ROWS, R, true, false>(in, out, n, m, s);
+        else launch_stream<K, LT, TM_ROWS, R, false, false>(in, out, n, m, s);
+    }
+}
+
+// One ROWS pass: strides 2^hi .. 2^(hi-R+1) of a level over n (virtual) keys.
+template <typename K, int LT>
+void launch_rows(const K* in, K* out, int64_t n, int hi, int R, bool flip, hipStream_t s) {
+    TileMap m{};
+    m.lo = hi - R + 1;
+    m.hi = hi;
+    m.logB = LT - R;
+    m.flip = flip;
+    const int64_t per_seg = ((int64_t)1 << m.lo) >> m.logB;
+    const int64_t full_segs = n >> (hi + 1);
+    const int64_t rem = n - (full_segs << (hi + 1));
+    int64_t part = (rem + ((int64_t)1 << m.logB) - 1) >> m.logB;
+    if (part > per_seg) part = per_seg;
+    m.ntiles = full_segs * per_seg + part;
+    switch (R) {
+        case 1: launch_rows_r<K, LT, 1>(in, out, n, m, s); break;
+        case 2: launch_rows_r<K, LT, 2>(in, out, n, m, s); break;
+        case 3: launch_rows_r<K, LT, 3>(in, out, n, m, s); break;
+        case 4: launch_rows_r<K, LT, 4>(in, out, n, m, s); break;
+        case 5: launch_rows_r<K, LT, 5>(in, out, n, m, s); break;
+        case 6: launch_rows_r<K, LT, 6>(in, out, n, m, s); break;
+        case 7: launch_rows_r<K, LT, 7>(in, out, n, m, s); break;
+        case 8: launch_rows_r<K, LT, 8>(in, out, n, m, s); break;
+        case 9: launch_rows_r<K, LT, 9>(in, out, n, m, s); break;
+        default: launch_rows_r<K, LT, 10>(in, out, n, m, s); break;
+    }
+}
+
+// One HBM pass of the plan.
+struct Pass {
+    Kind kind;  // KIND_TILE_SORT, KIND_GLOBAL (ROWS), KIND_TILE_MERGE
+    int hi, R;
+    bool flip;
+};
+
+// Pass plan for 2^k (virtual) keys: one SORT pass (levels 1..LT of each 2^LT
+// tile), then per level m > LT the strides 2^(m-1)..2^LT in near-equal ROWS
+// passes of <= rmax strides each, and one MERGE pass for the strides < 2^LT.
+inline std::vector<Pass> plan(int k, int LT, int rmax) {
+    std::vector<Pass> ps;
+    ps.push_back(Pass{KIND_TILE_SORT, LT - 1, 0, false});
+    for (int m = LT + 1; m <= k; ++m) {
+        const int x = m - LT;
+        const int parts = (x + rmax - 1) / rmax;
+        int hi = m - 1;
+        for (int p = 0; p < parts; ++p) {
+            const int R = x / parts + (p < x % parts ? 1 : 0);
+            ps.push_back(Pass{KIND_GLOBAL, hi, R, p == 0});
+            hi -= R;
+        }
+        ps.push_back(Pass{KIND_TILE_MERGE, LT - 1, 0, false});
+    }
+    return ps;
+}
+
+// LT: SORT/MERGE tile; LTR: ROWS tile.
+template <typename K, int LT, int LTR>
+hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
+                         LaunchHook* hook) {
+    const PlanKnobs& kn = plan_knobs();
+    const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
+    const std::vector<Pass> ps = plan(ceil_log2(n), LT, rmax);
+    const int np = (int)ps.size();
+    const bool pp = kn.pingpong && scratch != nullptr && scratch != out && scratch != in;
+    const double bytes = 2.0 * (double)n * sizeof(K);
+    TileMap tm{};
+    tm.ntiles = (n + (1 << LT) - 1) >> LT;
+    const K* src = in;
+    for (int i = 0; i < np; ++i) {
+        // ping-pong: pass i writes `out` iff an even number of passes follow it
+        K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
+        const Pass& p = ps[i];
+        HookScope hs(hook, p.kind, bytes, s);
+        if (p.kind == KIND_TILE_SORT) {
+            if constexpr (sizeof(K) == 8) {
+                if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
+                else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+            } else {
+                launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+            }
+        } else if (p.kind == KIND_GLOBAL) {
+            launch_rows<K, LTR>(src, dst, n, p.hi, p.R, p.flip, s);
+        } else {
+            launch_stream<K, LT, TM_MERGE, 0, false, false>(src, dst, n, tm, s);
+        }
+        src = dst;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Definition shared by sort_u32.hip / sort_u64.hip (one explicit instantiation each).
+template <typename K>
+hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
+                      LaunchHook* hook) {
+    if (n <= 0) return hipSuccess;
+    if (sizeof(K) == 4 && ord_in) return hipErrorInvalidValue;
+    constexpr int S = KT<K>::LT_SMALL;  // 14 (u32) / 13 (u64): the 64 KiB tile
+    const PlanKnobs& kn = plan_knobs();
+    const bool big = kn.tile_u32 == 15, rbig = kn.rows_tile_u32 == 15;
+    if (big && rbig) return local_sort_lt<K, S + 1, S + 1>(in, out, n, ord_in, scratch, s, hook);
+    if (big) return local_sort_lt<K, S + 1, S>(in, out, n, ord_in, scratch, s, hook);
+    return local_sort_lt<K, S, S>(in, out, n, ord_in, scratch, s, hook);
+}
+
+}  // namespace misort

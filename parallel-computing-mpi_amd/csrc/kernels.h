@@ -28,9 +28,11 @@ struct LaunchHook {
 // Local ascending sort of n keys: in -> out (in == out allowed).
 // K = uint32_t or uint64_t.  ord_in: the input holds IEEE doubles that are
 // mapped to order-preserving u64 on load (K must be uint64_t); the output
-// then stays in that ordered form.
+// then stays in that ordered form.  scratch (n keys, distinct from in and out,
+// or nullptr) lets the passes ping-pong between two buffers instead of
+// rewriting `out` in place (copy-shaped HBM traffic).
 template <typename K>
-hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, hipStream_t s,
+hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                       LaunchHook* hook);
 
 // Compare-split merge (device half of psort.cc:116-164): out[0..na) = the na

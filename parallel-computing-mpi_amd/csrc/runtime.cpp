@@ -296,7 +296,7 @@ struct misort_ctx {
     hipStream_t stream = nullptr;
     Transport* tr = nullptr;
     int nranks = 1, rank = 0;
-    DevBuf work, recv, scratch, small, samp_me, samp_peer;
+    DevBuf work, recv, scratch, small, samp_me, samp_peer, pong;
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     Profiler prof;
@@ -312,11 +312,16 @@ misort::LaunchHook* hook(misort_ctx* c) { return c->prof.on ? &c->prof : nullptr
 
 int do_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, bool ord_in,
                   hipStream_t s) {
+    // scratch for the ping-pong passes (grown on demand, kept for the context)
+    int rc = c->pong.ensure(std::max<size_t>(16, (size_t)n * key_bytes(dtype)));
+    if (rc) return rc;
     hipError_t e;
     if (dtype == MISORT_U32)
-        e = misort::local_sort<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, false, s, hook(c));
+        e = misort::local_sort<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, false, (uint32_t*)c->pong.p, s,
+                                         hook(c));
     else
-        e = misort::local_sort<uint64_t>((const uint64_t*)in, (uint64_t*)out, n, ord_in, s, hook(c));
+        e = misort::local_sort<uint64_t>((const uint64_t*)in, (uint64_t*)out, n, ord_in, (uint64_t*)c->pong.p, s,
+                                         hook(c));
     if (e != hipSuccess) return fail(MISORT_E_HIP, "local_sort: %s", hipGetErrorString(e));
     return MISORT_OK;
 }

@@ -1,0 +1,8 @@
+// sort_u32.hip -- local_sort<uint32_t> (the gfx950 bitonic tile engine of
+// bitonic.h), in its own translation unit so the key types compile in parallel.
+#include "bitonic.h"
+
+namespace misort {
+template hipError_t local_sort<uint32_t>(const uint32_t*, uint32_t*, int64_t, bool, uint32_t*, hipStream_t,
+                                        LaunchHook*);
+}  // namespace misort
