@@ -94,7 +94,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--logn", type=int, default=30, help="log2 of the total key count")
     ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
     ap.add_argument("--cpu-sample-logn", type=int, default=27)

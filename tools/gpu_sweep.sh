@@ -3,6 +3,8 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out
 i=0
+# throwaway warm-up (first run on a fresh box reads slow)
+timeout -k 10 120 python -u bench.py --logn 28 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/sw_warm.log 2>&1 || { tail -5 gpurun_out/sw_warm.log; exit 1; }
 for C in ${CONFIGS:-base}; do
   i=$((i+1))
   ENVS=$(echo "$C" | tr ',' ' '); [ "$C" = base ] && ENVS=""

@@ -4,7 +4,10 @@
 //   contig   tile = 2^LT consecutive keys (SORT/MERGE shape)
 //   rows R   tile = 2^R rows at stride 2^lo keys x 2^(LT-R) consecutive keys
 //            (ROWS shape, lo = hi-R+1, hi = 29)
-// Out of place (ping-pong) and in place.  Rate = 2 * 4 GiB / time.
+// Out of place (ping-pong) and in place, and three workgroup->tile maps:
+//   0 identity; 1 XCD-contiguous (workgroup b -> tile (b%8)*(T/8) + b/8, so
+//   each XCD streams its own 1/8 of the array, assuming round-robin dispatch);
+//   2 reversed tile order for odd passes.  Rate = 2 * 4 GiB / time.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/rows_probe.hip -o tools/bin/rows_probe
 #include <hip/hip_runtime.h>
 
@@ -34,8 +37,9 @@ __device__ __forceinline__ size_t gidx(size_t tile, int e, int R, int hi) {
 }
 
 template <bool NT_HINT>
-__global__ __launch_bounds__(NT) void tile_copy(const unsigned* in, unsigned* out, int R, int hi) {
-    const size_t tile = blockIdx.x;
+__global__ __launch_bounds__(NT) void tile_copy(const unsigned* in, unsigned* out, int R, int hi, int map) {
+    size_t tile = blockIdx.x;
+    if (map == 1) tile = (size_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
     u32x4 v[LOADS];
 #pragma unroll
     for (int k = 0; k < LOADS; ++k) {
@@ -63,11 +67,12 @@ int main() {
     CK(hipEventCreate(&e1));
     const unsigned grid = (unsigned)(n >> LT);
     for (int R = 0; R <= 10; ++R) {
-        for (int inplace = 0; inplace < 2; ++inplace) {
+        for (int map = 0; map < 2; ++map) {
+        for (int inplace = 0; inplace < 1; ++inplace) {
             for (int nt = 0; nt < 2; ++nt) {
                 auto go = [&] {
-                    if (nt) tile_copy<true><<<grid, NT>>>(a, inplace ? a : b, R, 29);
-                    else tile_copy<false><<<grid, NT>>>(a, inplace ? a : b, R, 29);
+                    if (nt) tile_copy<true><<<grid, NT>>>(a, inplace ? a : b, R, 29, map);
+                    else tile_copy<false><<<grid, NT>>>(a, inplace ? a : b, R, 29, map);
                 };
                 go();
                 CK(hipDeviceSynchronize());
@@ -78,10 +83,11 @@ int main() {
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 ms /= 5;
-                printf("{\"R\": %d, \"inplace\": %d, \"nt\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", R, inplace, nt, ms,
-                       2.0 * bytes / (ms * 1e-3) / 1e9);
+                printf("{\"R\": %d, \"map\": %d, \"inplace\": %d, \"nt\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", R, map,
+                       inplace, nt, ms, 2.0 * bytes / (ms * 1e-3) / 1e9);
                 fflush(stdout);
             }
+        }
         }
     }
     return 0;
