@@ -129,6 +129,15 @@ int misort_local_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
 /* Device half of compare_split_{max,min} (psort.cc:116-164) without the
  * exchange: d_out[0..nloc) = the nloc largest (keep_max=1) or smallest
  * (keep_max=0) keys of the sorted blocks local U recv, ascending. */
+/* psort.cc:377-490 parallel_quick_sort (the reference binary's shipped sort,
+ * called at psort.cc:647-648): d rounds of median-of-medians pivoting over
+ * shrinking hypercube sub-groups, RCCL send/recv with the partner, device merge.
+ * Per-rank output sizes are data-dependent, exactly as in the reference:
+ * *out_size receives this rank's count; MISORT_E_CAPACITY if it exceeds
+ * out_capacity (the reference allocates (loc+1)*P).  d_in is not modified. */
+int misort_parallel_quick_sort(misort_ctx* ctx, int dtype, const void* d_in, int64_t loc_size,
+                               void* d_out, int64_t out_capacity, int64_t* out_size, void* stream);
+
 int misort_merge_split(misort_ctx* ctx, int dtype, const void* d_local, int64_t nloc,
                        const void* d_recv, int64_t nrecv, void* d_out, int keep_max,
                        void* stream);

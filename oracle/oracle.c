@@ -239,6 +239,100 @@ int orc_parallel_bitonic_sort(int dtype, void *keys, int64_t n, int p) {
     return 0;
 }
 
+/* psort.cc:88-101 */
+static int64_t lower_bound_u64(const uint64_t *a, int64_t n, uint64_t x) {
+    int64_t low = 0, high = n;
+    while (low < high) {
+        int64_t mid = (low + high) / 2;
+        if (x <= a[mid]) high = mid;
+        else low = mid + 1;
+    }
+    return low;
+}
+
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* psort.cc:377-490, all P ranks in lockstep with the reference's literal
+ * buffer semantics: result_buffer holds (loc+1)*P keys, data beyond
+ * result_size is stale, and an empty rank's median is the stale
+ * result_buffer[0] (psort.cc:399; zero before anything was written).  Keys are
+ * carried as unsigned 64-bit (u32 widened, f64 through the order-preserving
+ * map: the same order as double compares except -0/+0 and NaN). */
+int orc_parallel_quick_sort(int dtype, const void *keys, int64_t n, int p, void *out,
+                            int64_t *sizes_out) {
+    if (p <= 0 || (p & (p - 1))) return -1; /* psort.cc:378-382 */
+    size_t w = dsize(dtype);
+    int64_t *rs = (int64_t *)malloc(sizeof(int64_t) * p);
+    int64_t *pi = (int64_t *)malloc(sizeof(int64_t) * p);
+    uint64_t *med = (uint64_t *)malloc(sizeof(uint64_t) * p);
+    uint64_t **buf = (uint64_t **)malloc(sizeof(uint64_t *) * p);
+    uint64_t **snd = (uint64_t **)malloc(sizeof(uint64_t *) * p);
+    int64_t *nsnd = (int64_t *)malloc(sizeof(int64_t) * p);
+    orc_block_sizes(n, p, rs);
+    const char *src = (const char *)keys;
+    for (int r = 0; r < p; ++r) {
+        int64_t cap = (rs[r] + 1) * p; /* psort.cc:385 */
+        buf[r] = (uint64_t *)calloc((size_t)cap, 8);
+        snd[r] = (uint64_t *)malloc((size_t)cap * 8);
+        for (int64_t k = 0; k < rs[r]; ++k, src += w) {
+            uint64_t v = 0;
+            memcpy(&v, src, w);
+            buf[r][k] = dtype == ORC_F64 ? f64_to_ord(v) : v;
+        }
+    }
+    int d = ilog2(p);
+    for (int i = 0; i < d; ++i) {
+        int g = p >> i, half = g >> 1;
+        for (int r = 0; r < p; ++r) {
+            radix_u64(buf[r], rs[r]);      /* psort.cc:398 */
+            med[r] = buf[r][rs[r] / 2];    /* psort.cc:399 */
+        }
+        for (int color = 0; color < p / g; ++color) { /* psort.cc:409-414 */
+            uint64_t *mb = (uint64_t *)malloc(sizeof(uint64_t) * g);
+            memcpy(mb, med + (size_t)color * g, sizeof(uint64_t) * g);
+            qsort(mb, (size_t)g, sizeof(uint64_t), cmp_u64);
+            uint64_t pivot = mb[g / 2];
+            for (int r = color * g; r < color * g + g; ++r)
+                pi[r] = lower_bound_u64(buf[r], rs[r], pivot); /* psort.cc:417 */
+            free(mb);
+        }
+        for (int r = 0; r < p; ++r) { /* what each rank sends (psort.cc:431-470) */
+            int low = (r % g) < half;
+            int64_t off = low ? pi[r] : 0;
+            nsnd[r] = low ? rs[r] - pi[r] : pi[r];
+            memcpy(snd[r], buf[r] + off, (size_t)nsnd[r] * 8);
+        }
+        for (int r = 0; r < p; ++r) {
+            int q = r ^ half, low = (r % g) < half;
+            if (low) { /* receive at pivot_index (psort.cc:444-452) */
+                memcpy(buf[r] + pi[r], snd[q], (size_t)nsnd[q] * 8);
+                rs[r] = pi[r] + nsnd[q];
+            } else { /* keep the upper part at the front, append (psort.cc:462-474) */
+                int64_t keep = rs[r] - pi[r];
+                memmove(buf[r], buf[r] + pi[r], (size_t)keep * 8);
+                memcpy(buf[r] + keep, snd[q], (size_t)nsnd[q] * 8);
+                rs[r] = keep + nsnd[q];
+            }
+        }
+    }
+    char *dst = (char *)out;
+    for (int r = 0; r < p; ++r) {
+        radix_u64(buf[r], rs[r]); /* psort.cc:485 */
+        sizes_out[r] = rs[r];
+        for (int64_t k = 0; k < rs[r]; ++k, dst += w) {
+            uint64_t v = dtype == ORC_F64 ? ord_to_f64(buf[r][k]) : buf[r][k];
+            memcpy(dst, &v, w);
+        }
+        free(buf[r]);
+        free(snd[r]);
+    }
+    free(rs); free(pi); free(med); free(buf); free(snd); free(nsnd);
+    return 0;
+}
+
 /* psort.cc:497-520.  The reference reads local_numbers[local_size-1] of an
  * empty block (UB); here an empty block contributes nothing and forwards the
  * previous boundary key. */

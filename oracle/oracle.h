@@ -52,6 +52,13 @@ int orc_parallel_bitonic_sort(int dtype, void *keys, int64_t n, int p);
  * keep_max[] for the d(d+1)/2 stages, returns the stage count. */
 int orc_bitonic_schedule(int p, int rank, int *partner, int *keep_max);
 
+/* psort.cc:377-490 -- parallel_quick_sort over P virtual ranks (input blocks
+ * in the reference layout, contiguous in rank order).  out receives the
+ * rank-ordered concatenation of the final blocks (n keys), sizes[r] the final
+ * block sizes (data-dependent).  Returns 0, or -1 when P is not a power of two. */
+int orc_parallel_quick_sort(int dtype, const void *keys, int64_t n, int p, void *out,
+                            int64_t *sizes);
+
 /* psort.cc:497-520 -- local descents plus rank-boundary descents. */
 int64_t orc_check_sort(int dtype, const void *keys, int64_t n, int p);
 

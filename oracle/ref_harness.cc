@@ -16,12 +16,17 @@
 //       reference's parallel_bitonic_sort(buffer, loc, N/P+1) (psort.cc:167).
 //       With PSORT_DUMP_DIR set, each rank writes its block before and after
 //       the sort as in_<r>_of_<P>.f64 / out_<r>_of_<P>.f64 (raw LE doubles).
+//       With PSORT_ALGO=quick the forwarder calls the reference's OWN
+//       parallel_quick_sort (psort.cc:377, found with dlsym(RTLD_NEXT)), i.e.
+//       the binary exactly as shipped, still with the dumps.
 //
 //   psort_ref --dtype u32|u64|f64 (--keys FILE | --gen-splitmix SEED --n N)
-//             [--out FILE] [--reps K]
-//       Our own MPI driver around the reference's parallel_bitonic_sort and
-//       check_sort (psort.cc:497), on the reference block layout
-//       (psort.cc:556-562).  Keys are carried as doubles: u32 exactly by value,
+//             [--out FILE] [--reps K] [--algo bitonic|quick]
+//       Our own MPI driver around the reference's parallel_bitonic_sort (or
+//       parallel_quick_sort, whose per-rank output sizes are data-dependent:
+//       the output file is the rank-ordered concatenation and the JSON line
+//       lists the sizes) and check_sort (psort.cc:497), on the reference block
+//       layout (psort.cc:556-562).  Keys are carried as doubles: u32 exactly by value,
 //       u64 by bit pattern (order-preserving only for keys <= 0x7FF0000000000000,
 //       checked), f64 as is.  Prints one JSON line with the max-over-ranks
 //       sort time (psort.cc:633-653 timed region) and the error count.
@@ -34,6 +39,7 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -56,11 +62,29 @@ static void dump(const char* tag, const double* a, int n) {
     fclose(f);
 }
 
+// The reference's own parallel_quick_sort (psort.cc:377): the next definition
+// of the symbol after this executable's interposer, i.e. libpsort_ref.so's.
+typedef double* (*quick_fn)(double*, int&, MPI_Comm);
+static quick_fn reference_quick_sort() {
+    static quick_fn f = (quick_fn)dlsym(RTLD_NEXT, "_Z19parallel_quick_sortPdRii");
+    if (!f) {
+        fprintf(stderr, "reference parallel_quick_sort not found: %s\n", dlerror());
+        MPI_Abort(MPI_COMM_WORLD, 4);
+    }
+    return f;
+}
+
+static bool algo_quick() {
+    const char* a = getenv("PSORT_ALGO");
+    return a && strcmp(a, "quick") == 0;
+}
+
 // Interposes psort.cc:377 at the call site psort.cc:647-648.
-double* parallel_quick_sort(double* buffer, int& loc_buf_size, MPI_Comm) {
+double* parallel_quick_sort(double* buffer, int& loc_buf_size, MPI_Comm comm) {
     int max_size = (int)(g_input_size / numprocs) + 1;  // psort.cc:556-557
     dump("in", buffer, loc_buf_size);
-    double* out = parallel_bitonic_sort(buffer, loc_buf_size, max_size);
+    double* out = algo_quick() ? reference_quick_sort()(buffer, loc_buf_size, comm)
+                               : parallel_bitonic_sort(buffer, loc_buf_size, max_size);
     // dump after the reference's own timer stops would be nicer, but the
     // forwarder only sees the sort; writing here adds file I/O to the
     // reference's printed sort time, so PSORT_DUMP_DIR runs are not timed runs.
@@ -90,6 +114,7 @@ static int keys_mode(int argc, char** argv) {
         else if (s == "--gen-splitmix") { gen = true; seed = strtoull(next().c_str(), nullptr, 0); }
         else if (s == "--n") n = atoll(next().c_str());
         else if (s == "--reps") reps = atoi(next().c_str());
+        else if (s == "--algo") setenv("PSORT_ALGO", next().c_str(), 1);
     }
     MPI_Init(&argc, &argv);
     MPI_Comm_size(MPI_COMM_WORLD, &numprocs);
@@ -143,7 +168,9 @@ static int keys_mode(int argc, char** argv) {
         }
         MPI_Barrier(MPI_COMM_WORLD);  // psort.cc:633
         double t0 = MPI_Wtime();
-        res = parallel_bitonic_sort(buf, iloc, max_size);
+        iloc = (int)loc;
+        res = algo_quick() ? reference_quick_sort()(buf, iloc, MPI_COMM_WORLD)
+                           : parallel_bitonic_sort(buf, iloc, max_size);
         double t = MPI_Wtime() - t0, tmax = 0;
         MPI_Reduce(&t, &tmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);  // psort.cc:652
         if (tmax < best) best = tmax;
@@ -151,22 +178,33 @@ static int keys_mode(int argc, char** argv) {
     }
     // check_sort prints "<k> errors in sorting" on rank 0 (psort.cc:518).
     check_sort(res, iloc);
+    // output sizes (quick sort moves keys between ranks) and rank offsets
+    long long oloc = iloc, ooff = 0;
+    MPI_Exscan(&oloc, &ooff, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
+    if (myid == 0) ooff = 0;
+    std::vector<long long> sizes(numprocs);
+    MPI_Gather(&oloc, 1, MPI_LONG_LONG, sizes.data(), 1, MPI_LONG_LONG, 0, MPI_COMM_WORLD);
     if (!out.empty()) {
-        for (long long k = 0; k < loc; ++k) {
-            if (w == 4) { uint32_t v = (uint32_t)res[k]; memcpy(&raw[k * 4], &v, 4); }
-            else memcpy(&raw[k * 8], &res[k], 8);
+        std::vector<unsigned char> ob((size_t)oloc * w + 8);
+        for (long long k = 0; k < oloc; ++k) {
+            if (w == 4) { uint32_t v = (uint32_t)res[k]; memcpy(&ob[k * 4], &v, 4); }
+            else memcpy(&ob[k * 8], &res[k], 8);
         }
         int ofd = open(out.c_str(), O_WRONLY | O_CREAT, 0644);
         if (ofd < 0) { perror(out.c_str()); MPI_Abort(MPI_COMM_WORLD, 2); }
-        if (loc > 0) {
-            ssize_t put = pwrite(ofd, raw.data(), (size_t)loc * w, (off_t)(off * (long long)w));
-            if (put != (ssize_t)(loc * w)) { fprintf(stderr, "short write\n"); MPI_Abort(MPI_COMM_WORLD, 2); }
+        if (oloc > 0) {
+            ssize_t put = pwrite(ofd, ob.data(), (size_t)oloc * w, (off_t)(ooff * (long long)w));
+            if (put != (ssize_t)(oloc * w)) { fprintf(stderr, "short write\n"); MPI_Abort(MPI_COMM_WORLD, 2); }
         }
         close(ofd);
     }
-    if (myid == 0)
-        printf("{\"n\": %lld, \"p\": %d, \"dtype\": \"%s\", \"sort_s\": %.6f, \"reps\": %d}\n",
-               n, numprocs, dtype.c_str(), best, reps);
+    if (myid == 0) {
+        std::string sz;
+        for (int r = 0; r < numprocs; ++r) sz += (r ? ", " : "") + std::to_string(sizes[r]);
+        printf("{\"n\": %lld, \"p\": %d, \"dtype\": \"%s\", \"algo\": \"%s\", \"sort_s\": %.6f, \"reps\": %d, "
+               "\"sizes\": [%s]}\n",
+               n, numprocs, dtype.c_str(), algo_quick() ? "quick" : "bitonic", best, reps, sz.c_str());
+    }
     delete[] res;
     MPI_Finalize();
     return 0;

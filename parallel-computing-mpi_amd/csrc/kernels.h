@@ -42,6 +42,18 @@ template <typename K>
 hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
                        int keep_max, int64_t* scratch, hipStream_t s, LaunchHook* hook);
 
+// Full merge of two ascending runs: out[0..na+nb) (A first on ties; for pure
+// keys the result equals std::sort of the concatenation).  scratch holds
+// ceil((na+nb)/2048)+1 int64 co-ranks.
+template <typename K>
+hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, int64_t* scratch, hipStream_t s,
+                      LaunchHook* hook);
+
+// psort.cc:88-101 lower_bound on a sorted device run: *d_out = first i with
+// x <= a[i], or n.
+template <typename K>
+hipError_t lower_bound(const K* a, int64_t n, K x, int64_t* d_out, hipStream_t s);
+
 // Local descents a[i] > a[i+1] (psort.cc:497-501), compared as T
 // (uint32_t, uint64_t or double); result added to *count (device u64).
 template <typename T>

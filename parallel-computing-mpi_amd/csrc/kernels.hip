@@ -130,6 +130,18 @@ __global__ void k_gather_samples(const K* __restrict__ a, int64_t n, int64_t str
     out[c] = a[x];
 }
 
+// psort.cc:88-101: first index i in [0, n) with x <= a[i] (n if none), one lane.
+template <typename K>
+__global__ void k_lower_bound(const K* __restrict__ a, int64_t n, K x, int64_t* __restrict__ out) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (x <= a[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    *out = lo;
+}
+
 __global__ void k_f64_ord(uint64_t* a, int64_t n, int to_ord) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -170,6 +182,25 @@ hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out, i
     k_merge_partition<K><<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, s>>>(a, na, b, nb, d0, na,
                                                                               ntiles, scratch);
     k_merge_tiles<K><<<(unsigned)ntiles, MS_NT, 0, s>>>(a, na, b, nb, d0, na, scratch, out);
+    return hipGetLastError();
+}
+
+template <typename K>
+hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, int64_t* scratch, hipStream_t s,
+                      LaunchHook* hook) {
+    const int64_t nout = na + nb;
+    if (nout <= 0) return hipSuccess;
+    const int64_t ntiles = (nout + MS_TILE - 1) / MS_TILE;
+    HookScope hs(hook, KIND_MERGE_SPLIT, 2.0 * (double)nout * sizeof(K), s);
+    k_merge_partition<K><<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, s>>>(a, na, b, nb, 0, nout, ntiles,
+                                                                              scratch);
+    k_merge_tiles<K><<<(unsigned)ntiles, MS_NT, 0, s>>>(a, na, b, nb, 0, nout, scratch, out);
+    return hipGetLastError();
+}
+
+template <typename K>
+hipError_t lower_bound(const K* a, int64_t n, K x, int64_t* d_out, hipStream_t s) {
+    k_lower_bound<K><<<1, 1, 0, s>>>(a, n, x, d_out);
     return hipGetLastError();
 }
 
@@ -217,6 +248,12 @@ template hipError_t merge_split<uint32_t>(const uint32_t*, int64_t, const uint32
                                           uint32_t*, int, int64_t*, hipStream_t, LaunchHook*);
 template hipError_t merge_split<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t,
                                           uint64_t*, int, int64_t*, hipStream_t, LaunchHook*);
+template hipError_t merge_full<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int64_t, uint32_t*,
+                                         int64_t*, hipStream_t, LaunchHook*);
+template hipError_t merge_full<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t, uint64_t*,
+                                         int64_t*, hipStream_t, LaunchHook*);
+template hipError_t lower_bound<uint32_t>(const uint32_t*, int64_t, uint32_t, int64_t*, hipStream_t);
+template hipError_t lower_bound<uint64_t>(const uint64_t*, int64_t, uint64_t, int64_t*, hipStream_t);
 template hipError_t count_descents<uint32_t>(const uint32_t*, int64_t, unsigned long long*,
                                              hipStream_t);
 template hipError_t count_descents<uint64_t>(const uint64_t*, int64_t, unsigned long long*,

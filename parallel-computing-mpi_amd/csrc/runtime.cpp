@@ -138,6 +138,10 @@ struct DevBuf {
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+    }
 };
 
 // ---------------------------------------------------------------- transport
@@ -297,6 +301,7 @@ struct misort_ctx {
     Transport* tr = nullptr;
     int nranks = 1, rank = 0;
     DevBuf work, recv, scratch, small, samp_me, samp_peer, pong;
+    DevBuf qa, qb, qcnt;  // quick sort: current run, merge target, exchanged counts
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     Profiler prof;
@@ -461,6 +466,92 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     }
     if (cur != out && loc > 0) HIPCHK(hipMemcpyAsync(out, cur, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
     if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, loc, s));
+    return MISORT_OK;
+}
+
+// psort.cc:377-490 parallel_quick_sort on the GPU: d rounds over shrinking
+// hypercube sub-groups; each round takes the median of medians of the group as
+// pivot and swaps the part below it (low half of the group) or at/above it
+// (high half) with the partner rank.  The reference re-sorts the whole buffer
+// each round (std::sort); the runs stay sorted here, so a device merge of the
+// kept part and the received part gives the same sequence.
+int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* out, int64_t out_cap,
+                   int64_t* out_n, hipStream_t s) {
+    if (!valid_dtype(dtype)) return fail(MISORT_E_INVALID, "bad dtype %d", dtype);
+    if (loc < 0) return fail(MISORT_E_INVALID, "negative loc_size");
+    const int p = c->nranks;
+    if (p & (p - 1)) return fail(MISORT_E_NOT_POW2, "Quick sort requires 2^d processors");  // psort.cc:378-382
+    const size_t w = key_bytes(dtype);
+    const bool f64 = dtype == MISORT_F64;
+    int rc;
+    if ((rc = c->qa.ensure(std::max<size_t>(16, (size_t)loc * w)))) return rc;
+    if ((rc = c->qcnt.ensure(64))) return rc;
+    if ((rc = do_local_sort(c, dtype, in, c->qa.p, loc, f64, s))) return rc;  // psort.cc:398
+    int64_t rs = loc;
+    uint64_t stale0 = 0;  // result_buffer[0] as last written: the median of an empty rank (psort.cc:399)
+    auto key_at = [&](int64_t i, uint64_t& v) -> int {  // one key of the current run, to the host
+        v = 0;
+        HIPCHK(hipMemcpyAsync(&v, (const char*)c->qa.p + (size_t)i * w, w, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return MISORT_OK;
+    };
+    const int d = ilog2(p);
+    for (int i = 0; i < d; ++i) {                       // psort.cc:389
+        const int g = p >> i, half = g >> 1;            // new_comm_size (psort.cc:392-403)
+        const int color = c->rank / g;                  // psort.cc:393
+        const bool low = (c->rank % g) < half;          // my_new_id < my_partner (psort.cc:431)
+        const int partner = c->rank ^ half;             // psort.cc:424
+        uint64_t med = stale0;
+        if (rs > 0) {
+            if ((rc = key_at(0, stale0))) return rc;
+            if ((rc = key_at(rs / 2, med))) return rc;  // my_median = result_buffer[rs/2] (psort.cc:399)
+        }
+        std::vector<int64_t> all(1, (int64_t)med);
+        const int64_t mine = (int64_t)med;
+        if (p > 1 && (rc = c->tr->allgather_i64(&mine, 1, all, s))) return rc;  // psort.cc:409-410
+        std::vector<uint64_t> grp(all.begin() + (size_t)color * g, all.begin() + (size_t)color * g + g);
+        std::sort(grp.begin(), grp.end());                                      // psort.cc:413
+        const uint64_t pivot = grp[g / 2];                                      // psort.cc:414
+        int64_t* dcnt = (int64_t*)c->qcnt.p;
+        hipError_t e = w == 4 ? misort::lower_bound<uint32_t>((const uint32_t*)c->qa.p, rs, (uint32_t)pivot, dcnt, s)
+                              : misort::lower_bound<uint64_t>((const uint64_t*)c->qa.p, rs, pivot, dcnt, s);
+        if (e != hipSuccess) return fail(MISORT_E_HIP, "lower_bound: %s", hipGetErrorString(e));
+        int64_t pi = 0;                                                         // psort.cc:417
+        HIPCHK(hipMemcpyAsync(&pi, dcnt, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        // low half keeps [0, pi) and sends [pi, rs); high half keeps [pi, rs), sends [0, pi)
+        const int64_t keep_off = low ? 0 : pi, keep_n = low ? pi : rs - pi;
+        const int64_t send_off = low ? pi : 0, send_n = low ? rs - pi : pi;
+        // MPI_Send/MPI_Recv + MPI_Get_count (psort.cc:438-471): counts first, then keys
+        HIPCHK(hipMemcpyAsync(dcnt, &send_n, 8, hipMemcpyHostToDevice, s));
+        if ((rc = c->tr->sendrecv(dcnt, 8, dcnt + 1, 8, partner, s))) return rc;
+        int64_t recv_n = 0;
+        HIPCHK(hipMemcpyAsync(&recv_n, dcnt + 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = c->recv.ensure(std::max<size_t>(16, (size_t)recv_n * w)))) return rc;
+        if ((rc = c->tr->sendrecv((const char*)c->qa.p + (size_t)send_off * w, (size_t)send_n * w, c->recv.p,
+                                  (size_t)recv_n * w, partner, s)))
+            return rc;
+        const int64_t nn = keep_n + recv_n;
+        if ((rc = c->qb.ensure(std::max<size_t>(16, (size_t)nn * w)))) return rc;
+        if ((rc = c->scratch.ensure((size_t)((nn + 2047) / 2048 + 2) * sizeof(int64_t)))) return rc;
+        const char* kp = (const char*)c->qa.p + (size_t)keep_off * w;
+        e = w == 4 ? misort::merge_full<uint32_t>((const uint32_t*)kp, keep_n, (const uint32_t*)c->recv.p, recv_n,
+                                                  (uint32_t*)c->qb.p, (int64_t*)c->scratch.p, s, hook(c))
+                   : misort::merge_full<uint64_t>((const uint64_t*)kp, keep_n, (const uint64_t*)c->recv.p, recv_n,
+                                                  (uint64_t*)c->qb.p, (int64_t*)c->scratch.p, s, hook(c));
+        if (e != hipSuccess) return fail(MISORT_E_HIP, "merge: %s", hipGetErrorString(e));
+        c->qa.swap(c->qb);
+        rs = nn;
+        c->xchg_stages += 1;
+        c->xchg_bytes += (int64_t)((send_n + recv_n) * w);
+    }
+    *out_n = rs;                                                                // psort.cc:486
+    if (rs > out_cap)
+        return fail(MISORT_E_CAPACITY, "quick sort result of %lld keys exceeds the output capacity %lld",
+                    (long long)rs, (long long)out_cap);
+    if (rs > 0) HIPCHK(hipMemcpyAsync(out, c->qa.p, (size_t)rs * w, hipMemcpyDeviceToDevice, s));
+    if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, rs, s));
     return MISORT_OK;
 }
 
@@ -663,6 +754,14 @@ int misort_parallel_bitonic_sort_oop(misort_ctx* c, int dtype, const void* in, v
 int misort_parallel_bitonic_sort(misort_ctx* c, int dtype, void* keys, int64_t loc,
                                  int64_t max_size, void* stream) {
     return misort_parallel_bitonic_sort_oop(c, dtype, keys, keys, loc, max_size, stream);
+}
+
+int misort_parallel_quick_sort(misort_ctx* c, int dtype, const void* in, int64_t loc, void* out,
+                               int64_t out_capacity, int64_t* out_size, void* stream) {
+    if (!c || !out_size) return fail(MISORT_E_INVALID, "null argument");
+    if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
+    if ((loc > 0 && !in) || (out_capacity > 0 && !out)) return fail(MISORT_E_INVALID, "null buffer");
+    return parallel_quick(c, dtype, in, loc, out, out_capacity, out_size, pick(c, stream));
 }
 
 int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc, const void* recv,

@@ -76,6 +76,7 @@ def lib():
         "misort_parallel_bitonic_sort_oop": ([vp, i32, vp, vp, i64, i64, vp], i32),
         "misort_local_sort": ([vp, i32, vp, vp, i64, vp], i32),
         "misort_merge_split": ([vp, i32, vp, i64, vp, i64, vp, i32, vp], i32),
+        "misort_parallel_quick_sort": ([vp, i32, vp, i64, vp, i64, ctypes.POINTER(i64), vp], i32),
         "misort_check_sort": ([vp, i32, vp, i64, ctypes.POINTER(i64), vp], i32),
         "misort_sort_host": ([vp, i32, vp, vp, i64, i64], i32),
         "misort_fill_splitmix": ([vp, i32, vp, i64, ctypes.c_uint64, i64, vp], i32),
@@ -276,6 +277,19 @@ class Context:
         _check(lib().misort_parallel_bitonic_sort_oop(self._h, dt, _ptr(buffer), _ptr(out), loc,
                                                       mx, self._stream(stream)))
         return out
+
+    def parallel_quick_sort(self, buffer, loc_buf_size=None, out=None, stream=None):
+        """psort.cc:377 (the reference binary's shipped sort).  Returns
+        ``(out, n)``: this rank's sorted keys are ``out[:n]``, n data-dependent.
+        ``out`` defaults to the reference's capacity, (loc+1)*P keys."""
+        import torch
+        loc = buffer.numel() if loc_buf_size is None else int(loc_buf_size)
+        if out is None:
+            out = torch.empty((loc + 1) * self.numprocs, dtype=buffer.dtype, device=buffer.device)
+        n = ctypes.c_int64()
+        _check(lib().misort_parallel_quick_sort(self._h, _dtype_of(buffer), _ptr(buffer), loc, _ptr(out),
+                                                out.numel(), ctypes.byref(n), self._stream(stream)))
+        return out, int(n.value)
 
     def local_sort(self, inp, out=None, n=None, stream=None):
         """psort.cc:175 (std::sort of the local block) on the GPU."""

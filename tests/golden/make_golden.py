@@ -15,6 +15,9 @@ oracle/ref_harness.cc for how it drives psort.cc without modifying it):
 * "keys": the reference's parallel_bitonic_sort on a given key set (u32
   SplitMix64 keys, and u64 duplicate-heavy/skewed keys carried as
   order-preserving doubles).
+* algo "quick": the same two kinds with the reference's OWN parallel_quick_sort
+  (psort.cc:377, the binary as shipped); per-rank output sizes are
+  data-dependent and recorded.
 
 Stored: a JSON manifest (sizes, error counts, stdout, SHA-256 of inputs and of
 the rank-ordered outputs, head/tail keys) plus raw little-endian arrays for the
@@ -55,9 +58,9 @@ def run(cmd, env=None):
     return r.stdout
 
 
-def psort_case(n, p):
+def psort_case(n, p, algo="bitonic"):
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, PSORT_DUMP_DIR=d)
+        env = dict(os.environ, PSORT_DUMP_DIR=d, PSORT_ALGO=algo)
         out = run([O.MPIRUN, "-np", str(p), REF, str(n)], env=env)
         ins = [np.fromfile(f"{d}/in_{r}_of_{p}.f64") for r in range(p)]
         outs = [np.fromfile(f"{d}/out_{r}_of_{p}.f64") for r in range(p)]
@@ -66,7 +69,7 @@ def psort_case(n, p):
     stable = [l for l in lines if "required" not in l and "sort time" not in l]
     x, y = np.concatenate(ins), np.concatenate(outs)
     case = {
-        "mode": "psort", "n": n, "p": p,
+        "mode": "psort", "algo": algo, "n": n, "p": p,
         "sizes": [int(b.size) for b in outs],
         "errors": errors, "stdout_stable": stable,
         "in_sha256": sha(x), "out_sha256": sha(y),
@@ -74,23 +77,27 @@ def psort_case(n, p):
     }
     if n <= FULL_LIMIT:
         x.tofile(os.path.join(HERE, f"psort_in_N{n}.f64"))
-        y.tofile(os.path.join(HERE, f"psort_out_N{n}_P{p}.f64"))
+        tag = "" if algo == "bitonic" else algo + "_"
+        y.tofile(os.path.join(HERE, f"psort_{tag}out_N{n}_P{p}.f64"))
     return case
 
 
-def keys_case(name, keys, p, dtype, store_full):
+def keys_case(name, keys, p, dtype, store_full, algo="bitonic"):
     with tempfile.TemporaryDirectory() as d:
         kf, of = f"{d}/keys.bin", f"{d}/out.bin"
         keys.tofile(kf)
-        out = run([O.MPIRUN, "-np", str(p), REF, "--dtype", dtype, "--keys", kf, "--out", of])
+        out = run([O.MPIRUN, "-np", str(p), REF, "--dtype", dtype, "--keys", kf, "--out", of,
+                   "--algo", algo])
         y = np.fromfile(of, dtype=keys.dtype)
     errors = int([l for l in out.splitlines() if "errors in sorting" in l][0].split()[0])
+    info = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     case = {
-        "mode": "keys", "name": name, "dtype": dtype, "n": int(keys.size), "p": p,
-        "errors": errors, "in_sha256": sha(keys), "out_sha256": sha(y),
+        "mode": "keys", "algo": algo, "name": name, "dtype": dtype, "n": int(keys.size), "p": p,
+        "errors": errors, "sizes": info["sizes"], "in_sha256": sha(keys), "out_sha256": sha(y),
     }
     if store_full:
-        y.tofile(os.path.join(HERE, f"keys_{name}_P{p}.out"))
+        tag = "" if algo == "bitonic" else algo + "_"
+        y.tofile(os.path.join(HERE, f"keys_{tag}{name}_P{p}.out"))
     return case
 
 
@@ -135,9 +142,28 @@ def main():
             c = keys_case(f"u64mix_n{n}", keys, p, "u64", store_full=True)
             print(f"keys u64 N={n} P={p} errors={c['errors']}", flush=True)
             cases.append(c)
+    # the shipped sort: parallel_quick_sort
+    for n in [13, 100, 1024, 1031, 65537, 1000003]:
+        for p in PS:
+            c = psort_case(n, p, "quick")
+            print(f"psort quick N={n} P={p} sizes={c['sizes']} errors={c['errors']}", flush=True)
+            cases.append(c)
+    for n in [1000, 4099, 65541]:
+        keys = O.splitmix(0x5EED0001, n, np.uint32)
+        for p in PS:
+            c = keys_case(f"u32_n{n}", keys, p, "u32", store_full=n <= 4099, algo="quick")
+            print(f"keys quick u32 N={n} P={p} sizes={c['sizes']}", flush=True)
+            cases.append(c)
+    for n in [5003, 20011]:
+        keys = mixed_u64(n, 0x5EED0005 + n)
+        for p in PS:
+            c = keys_case(f"u64mix_n{n}", keys, p, "u64", store_full=True, algo="quick")
+            print(f"keys quick u64 N={n} P={p} sizes={c['sizes']}", flush=True)
+            cases.append(c)
     meta = {
         "generator": "tests/golden/make_golden.py",
-        "reference": "Parallel-Sorting/src/psort.cc (unmodified; parallel_bitonic_sort via oracle/_ref)",
+        "reference": "Parallel-Sorting/src/psort.cc (unmodified; parallel_bitonic_sort and "
+                     "parallel_quick_sort via oracle/_ref)",
         "mpi": "MPICH 3.3.2 (/opt/conda), g++ 11, -g -O1",
         "cases": cases,
     }

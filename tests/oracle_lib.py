@@ -39,6 +39,8 @@ def lib():
         L.orc_parallel_bitonic_sort.restype = ctypes.c_int
         L.orc_bitonic_schedule.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp]
         L.orc_bitonic_schedule.restype = ctypes.c_int
+        L.orc_parallel_quick_sort.argtypes = [ctypes.c_int, vp, i64, ctypes.c_int, vp, vp]
+        L.orc_parallel_quick_sort.restype = ctypes.c_int
         L.orc_check_sort.argtypes = [ctypes.c_int, vp, i64, ctypes.c_int]
         L.orc_check_sort.restype = ctypes.c_int64
         _lib = L
@@ -96,6 +98,17 @@ def parallel_bitonic_sort(keys, p):
     if rc != 0:
         raise ValueError("bitonic sort requires 2^d processors")
     return keys
+
+
+def parallel_quick_sort(keys, p):
+    """All P ranks of psort.cc:377-490: (rank-ordered output, per-rank sizes)."""
+    keys = np.ascontiguousarray(keys)
+    out = np.empty_like(keys)
+    sizes = np.zeros(p, dtype=np.int64)
+    rc = lib().orc_parallel_quick_sort(dtype_code(keys), _ptr(keys), keys.size, p, _ptr(out), _ptr(sizes))
+    if rc != 0:
+        raise ValueError("Quick sort requires 2^d processors")
+    return out, sizes
 
 
 def schedule(p, rank):

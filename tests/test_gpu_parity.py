@@ -152,8 +152,8 @@ def virtual_ranks(ctx, x, p):
     return np.concatenate([to_host(b, x.dtype) for b in blocks])
 
 
-PSORT = [c for c in GOLD if c["mode"] == "psort"]
-KEYS = [c for c in GOLD if c["mode"] == "keys"]
+PSORT = [c for c in GOLD if c["mode"] == "psort" and c.get("algo", "bitonic") == "bitonic"]
+KEYS = [c for c in GOLD if c["mode"] == "keys" and c.get("algo", "bitonic") == "bitonic"]
 
 
 @pytest.mark.parametrize("case", PSORT, ids=lambda c: f"N{c['n']}_P{c['p']}")

@@ -18,8 +18,10 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-PSORT = [c for c in GOLD if c["mode"] == "psort"]
-KEYS = [c for c in GOLD if c["mode"] == "keys"]
+PSORT = [c for c in GOLD if c["mode"] == "psort" and c.get("algo", "bitonic") == "bitonic"]
+KEYS = [c for c in GOLD if c["mode"] == "keys" and c.get("algo", "bitonic") == "bitonic"]
+QPSORT = [c for c in GOLD if c["mode"] == "psort" and c.get("algo") == "quick"]
+QKEYS = [c for c in GOLD if c["mode"] == "keys" and c.get("algo") == "quick"]
 
 
 @pytest.mark.parametrize("case", PSORT, ids=lambda c: f"N{c['n']}_P{c['p']}")
@@ -60,9 +62,33 @@ def test_keys_cases(case):
     assert O.check_sort(y, case["p"]) == case["errors"]
 
 
+@pytest.mark.parametrize("case", QPSORT, ids=lambda c: f"N{c['n']}_P{c['p']}")
+def test_psort_quick_sort(case):
+    # psort.cc:377-490 as shipped: per-rank sizes are data-dependent.
+    n, p = case["n"], case["p"]
+    x = O.generate_f64(n)
+    assert sha(x) == case["in_sha256"]
+    y, sizes = O.parallel_quick_sort(x, p)
+    assert sizes.tolist() == case["sizes"]
+    assert sha(y) == case["out_sha256"]
+    full = os.path.join(GOLD_DIR, f"psort_quick_out_N{n}_P{p}.f64")
+    if os.path.exists(full):
+        np.testing.assert_array_equal(np.fromfile(full).view(np.uint64), y.view(np.uint64))
+
+
+@pytest.mark.parametrize("case", QKEYS, ids=lambda c: f"{c['name']}_P{c['p']}")
+def test_keys_quick_cases(case):
+    x = _keys_input(case)
+    y, sizes = O.parallel_quick_sort(x, case["p"])
+    assert sizes.tolist() == case["sizes"]
+    assert sha(y) == case["out_sha256"]
+
+
 def test_non_power_of_two_rejected():
     with pytest.raises(ValueError):
         O.parallel_bitonic_sort(np.arange(10, dtype=np.uint32), 3)
+    with pytest.raises(ValueError):
+        O.parallel_quick_sort(np.arange(10, dtype=np.uint32), 6)
 
 
 def test_schedule_matches_reference_loop():
@@ -84,4 +110,4 @@ def test_defective_layout_is_reproduced():
     # uneven blocks with P>=4 are not globally sorted by the
     # reference; the fixtures hold nonzero error counts and the oracle matches.
     bad = [c for c in GOLD if c["errors"] > 0]
-    assert bad and all(c["p"] >= 4 for c in bad)
+    assert bad and all(c["p"] >= 4 and c.get("algo", "bitonic") == "bitonic" for c in bad)
