@@ -17,6 +17,9 @@
 // reported separately with --verbose.
 //
 // Extensions (not in the reference; off by default):
+//   --algo bitonic|quick              bitonic (default, psort.cc:167) or the
+//                                     binary's shipped parallel_quick_sort
+//                                     (psort.cc:377; data-dependent block sizes)
 //   --keys FILE --dtype u32|u64|f64   sort a raw little-endian key file
 //   --out FILE                        write the rank-ordered result
 //   --verbose                         extra timing lines on stderr
@@ -81,9 +84,12 @@ static double get_timer() {
         }                                                                           \
     } while (0)
 
+static bool g_quick = false;
+
 static void misort_ok(int rc, const char* what) {
-    if (rc == MISORT_E_NOT_POW2) {  // psort.cc:168-172
-        std::cerr << "bitonic sort requires 2^d processors" << endl;
+    if (rc == MISORT_E_NOT_POW2) {  // psort.cc:168-172 / 378-382
+        std::cerr << (g_quick ? "Quick sort requires 2^d processors" : "bitonic sort requires 2^d processors")
+                  << endl;
         MPI_Abort(MPI_COMM_WORLD, -1);
         abort();
     }
@@ -143,6 +149,7 @@ int main(int argc, char** argv) {
         else if (s == "--out" && a + 1 < argc) out_file = argv[++a];
         else if (s == "--dtype" && a + 1 < argc) dtype_s = argv[++a];
         else if (s == "--verbose") verbose = true;
+        else if (s == "--algo" && a + 1 < argc) g_quick = std::string(argv[++a]) == "quick";
         else if (s[0] != '-') input_size = atoll(s.c_str());
     }
     const int dtype = dtype_s == "u32" ? MISORT_U32 : dtype_s == "u64" ? MISORT_U64 : MISORT_F64;
@@ -203,8 +210,12 @@ int main(int argc, char** argv) {
     }
 
     hipStream_t st = (hipStream_t)misort_stream(ctx);
+    // quick sort moves keys between ranks: the reference's (loc+1)*P capacity (psort.cc:385)
+    const long long cap = g_quick ? (local_input_size + 1) * numprocs : max_local_size;
     void* d_keys = nullptr;
+    void* d_out = nullptr;
     HIP_OK(hipMalloc(&d_keys, std::max<size_t>(16, (size_t)max_local_size * w)));
+    if (g_quick) HIP_OK(hipMalloc(&d_out, std::max<size_t>(16, (size_t)cap * w)));
     double t_h2d = MPI_Wtime();
     HIP_OK(hipMemcpyAsync(d_keys, host.data(), (size_t)local_input_size * w, hipMemcpyHostToDevice, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -212,36 +223,50 @@ int main(int argc, char** argv) {
 
     MPI_Barrier(MPI_COMM_WORLD);  // psort.cc:633
     get_timer();
-    misort_ok(misort_parallel_bitonic_sort(ctx, dtype, d_keys, local_input_size, max_local_size, st),
-              "parallel_bitonic_sort");
+    long long out_size = local_input_size;
+    if (g_quick) {
+        int64_t n_out = 0;
+        misort_ok(misort_parallel_quick_sort(ctx, dtype, d_keys, local_input_size, d_out, cap, &n_out, st),
+                  "parallel_quick_sort");
+        out_size = n_out;
+    } else {
+        misort_ok(misort_parallel_bitonic_sort(ctx, dtype, d_keys, local_input_size, max_local_size, st),
+                  "parallel_bitonic_sort");
+    }
     HIP_OK(hipStreamSynchronize(st));
     double par_sort_time = get_timer();  // psort.cc:650-656
     MPI_Reduce(&par_sort_time, &max_time, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
     if (myid == 0) cout << "parallel sort time = " << max_time << endl;
 
+    void* d_res = g_quick ? d_out : d_keys;
     int64_t errors = 0;  // psort.cc:659 -> 497-520
-    misort_ok(misort_check_sort(ctx, dtype, d_keys, local_input_size, &errors, st), "check_sort");
+    misort_ok(misort_check_sort(ctx, dtype, d_res, out_size, &errors, st), "check_sort");
     if (myid == 0) cout << errors << " errors in sorting" << endl;
 
     if (!out_file.empty() || verbose) {
+        long long out_off = 0;  // rank-ordered concatenation
+        MPI_Exscan(&out_size, &out_off, 1, MPI_LONG_LONG, MPI_SUM, MPI_COMM_WORLD);
+        if (myid == 0) out_off = 0;
+        if ((size_t)out_size * w + 8 > host.size()) host.resize((size_t)out_size * w + 8);
         double t_d2h = MPI_Wtime();
-        HIP_OK(hipMemcpyAsync(host.data(), d_keys, (size_t)local_input_size * w, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(host.data(), d_res, (size_t)out_size * w, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         t_d2h = MPI_Wtime() - t_d2h;
         if (!out_file.empty()) {
             int ofd = open(out_file.c_str(), O_WRONLY | O_CREAT, 0644);
-            if (ofd < 0 || (local_input_size > 0 &&
-                            pwrite(ofd, host.data(), (size_t)local_input_size * w,
-                                   (off_t)(offset * (long long)w)) != (ssize_t)(local_input_size * w))) {
+            if (ofd < 0 || (out_size > 0 &&
+                            pwrite(ofd, host.data(), (size_t)out_size * w, (off_t)(out_off * (long long)w)) !=
+                                (ssize_t)(out_size * w))) {
                 perror(out_file.c_str());
                 MPI_Abort(MPI_COMM_WORLD, 2);
             }
             close(ofd);
         }
         if (verbose)
-            fprintf(stderr, "rank %d device %d: %lld keys, h2d %.6f s, d2h %.6f s\n", myid, dev,
-                    local_input_size, t_h2d, t_d2h);
+            fprintf(stderr, "rank %d device %d: %lld keys in, %lld out, h2d %.6f s, d2h %.6f s\n", myid, dev,
+                    local_input_size, out_size, t_h2d, t_d2h);
     }
+    if (d_out) HIP_OK(hipFree(d_out));
     HIP_OK(hipFree(d_keys));
     misort_destroy(ctx);
     MPI_Finalize();
