@@ -97,6 +97,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--logn", type=int, default=30, help="log2 of the total key count")
     ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
+    ap.add_argument("--algo", choices=["bitonic", "sample"], default="bitonic",
+                    help="bitonic = psort.cc:167 (the metric); sample = psort.cc:203-375 redesigned")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N>1: skip the extra sample-sort timing reported under 'alt'")
     ap.add_argument("--cpu-sample-logn", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
@@ -143,8 +147,30 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def run(algo):
+        if algo == "sample":
+            ctx.parallel_sample_sort(d_in, loc, max_size, out=d_out, stream=stream.cuda_stream)
+        else:
+            ctx.parallel_bitonic_sort(d_in, loc, max_size, out=d_out, stream=stream.cuda_stream)
+
     def step():
-        ctx.parallel_bitonic_sort(d_in, loc, max_size, out=d_out, stream=stream.cuda_stream)
+        run(args.algo)
+
+    def timed(algo, steps):
+        """warm, then barrier + sync around `steps` sorts; max over ranks (s)."""
+        run(algo)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(algo)
+        torch.cuda.synchronize()
+        barrier()
+        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
 
     for _ in range(args.warmup):
         step()
@@ -171,6 +197,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     errors = ctx.check_sort(d_out, loc)  # psort.cc:497-520 over all ranks
+    alt = None
+    if world > 1 and args.algo == "bitonic" and not args.no_alt:
+        # the redesigned sample sort (one RCCL all-to-all) on the same input, same contract
+        ts = timed("sample", args.steps)
+        alt = {"sample_sort": {"value": n_total * args.steps / ts / 1e9, "unit": "Gkeys/s",
+                               "ms_per_step": ts / args.steps * 1e3,
+                               "check_errors": ctx.check_sort(d_out, loc),
+                               "note": "psort.cc:203-375 redesigned: samples, one all-to-all-v, "
+                                       "merge tree, rebalance to the reference layout"}}
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -190,7 +225,10 @@ def main():
             "config": {"workload": f"bitonic sort 2^{args.logn} {args.dtype} keys "
                                    f"(BASELINE config {'3/4' if args.logn == 30 else 'custom'})",
                        "keys": n_total, "keys_per_gpu": loc,
-                       "parallelism": f"hypercube bitonic, {world} GPU(s), RCCL compare-split"},
+                       "algo": args.algo,
+                       "parallelism": (f"hypercube bitonic, {world} GPU(s), RCCL compare-split"
+                                       if args.algo == "bitonic" else
+                                       f"sample sort, {world} GPU(s), RCCL all-to-all")},
             "check_errors": errors,
         }
         if world > 1:
@@ -218,6 +256,8 @@ def main():
                                "avg_launch_us": tms / nl * 1e3}
             kt = sum(v[1] for v in kern.values()) / args.steps
             out["kernel_ms_per_step"] = kt
+        if alt:
+            out["alt"] = alt
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -138,6 +138,18 @@ int misort_local_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
 int misort_parallel_quick_sort(misort_ctx* ctx, int dtype, const void* d_in, int64_t loc_size,
                                void* d_out, int64_t out_capacity, int64_t* out_size, void* stream);
 
+/* psort.cc:203-375 parallel_sample_native_sort / parallel_sample_bitonic_sort,
+ * redesigned for RCCL over xGMI: local sort, all-gathered regular samples,
+ * (key, rank, position) splitters, ONE all-to-all-v (every GPU pair on its
+ * own link), a device merge tree, and a rebalancing all-to-all-v into the
+ * reference block layout.  Same contract as misort_parallel_bitonic_sort_oop
+ * (d_out receives loc_size keys: the globally sorted sequence in the callers'
+ * block sizes); d_in != d_out.  The reference's versions are not well defined
+ * (an uninitialised splitter at :318, MPI_INT used for doubles at :224/:269),
+ * so parity is anchored on the sorted sequence, not on their per-rank sizes. */
+int misort_parallel_sample_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
+                                int64_t loc_size, int64_t max_size, void* stream);
+
 int misort_merge_split(misort_ctx* ctx, int dtype, const void* d_local, int64_t nloc,
                        const void* d_recv, int64_t nrecv, void* d_out, int keep_max,
                        void* stream);

@@ -54,6 +54,11 @@ hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, in
 template <typename K>
 hipError_t lower_bound(const K* a, int64_t n, K x, int64_t* d_out, hipStream_t s);
 
+// lb[v] / ub[v] = first index with a[i] >= vals[v] / a[i] > vals[v] in a
+// sorted run (device arrays of nv entries).
+template <typename K>
+hipError_t bounds(const K* a, int64_t n, const K* vals, int nv, int64_t* lb, int64_t* ub, hipStream_t s);
+
 // Local descents a[i] > a[i+1] (psort.cc:497-501), compared as T
 // (uint32_t, uint64_t or double); result added to *count (device u64).
 template <typename T>

@@ -142,6 +142,29 @@ __global__ void k_lower_bound(const K* __restrict__ a, int64_t n, K x, int64_t* 
     *out = lo;
 }
 
+// lower and upper bound of nv values in a sorted run, one lane per value.
+template <typename K>
+__global__ void k_bounds(const K* __restrict__ a, int64_t n, const K* __restrict__ vals, int nv,
+                         int64_t* __restrict__ lb, int64_t* __restrict__ ub) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nv) return;
+    const K x = vals[v];
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {  // first a[i] >= x
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    lb[v] = lo;
+    hi = n;
+    while (lo < hi) {  // first a[i] > x
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    ub[v] = lo;
+}
+
 __global__ void k_f64_ord(uint64_t* a, int64_t n, int to_ord) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -204,6 +227,13 @@ hipError_t lower_bound(const K* a, int64_t n, K x, int64_t* d_out, hipStream_t s
     return hipGetLastError();
 }
 
+template <typename K>
+hipError_t bounds(const K* a, int64_t n, const K* vals, int nv, int64_t* lb, int64_t* ub, hipStream_t s) {
+    if (nv <= 0) return hipSuccess;
+    k_bounds<K><<<(unsigned)((nv + 63) / 64), 64, 0, s>>>(a, n, vals, nv, lb, ub);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t count_descents(const T* a, int64_t n, unsigned long long* count, hipStream_t s) {
     if (n < 2) return hipSuccess;
@@ -252,6 +282,10 @@ template hipError_t merge_full<uint32_t>(const uint32_t*, int64_t, const uint32_
                                          int64_t*, hipStream_t, LaunchHook*);
 template hipError_t merge_full<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t, uint64_t*,
                                          int64_t*, hipStream_t, LaunchHook*);
+template hipError_t bounds<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int, int64_t*, int64_t*,
+                                     hipStream_t);
+template hipError_t bounds<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int, int64_t*, int64_t*,
+                                     hipStream_t);
 template hipError_t lower_bound<uint32_t>(const uint32_t*, int64_t, uint32_t, int64_t*, hipStream_t);
 template hipError_t lower_bound<uint64_t>(const uint64_t*, int64_t, uint64_t, int64_t*, hipStream_t);
 template hipError_t count_descents<uint32_t>(const uint32_t*, int64_t, unsigned long long*,

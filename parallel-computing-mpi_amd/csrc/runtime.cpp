@@ -160,6 +160,10 @@ struct Transport {
     // device buffers; both sides know both byte counts
     virtual int sendrecv(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, int peer,
                          hipStream_t s) = 0;
+    // all-to-all-v on device buffers: to rank q go send[soff[q], +scnt[q]) bytes,
+    // from rank q come recv[roff[q], +rcnt[q]); every rank knows its own counts
+    virtual int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv,
+                          const int64_t* roff, const int64_t* rcnt, hipStream_t s) = 0;
 };
 
 struct RcclTransport final : Transport {
@@ -187,6 +191,22 @@ struct RcclTransport final : Transport {
         NCCLCHK(ncclGroupEnd());
         return MISORT_OK;
     }
+    // One grouped call: every peer pair moves over its own xGMI link at once.
+    int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv, const int64_t* roff,
+                  const int64_t* rcnt, hipStream_t s) override {
+        if (scnt[rank] != rcnt[rank]) return fail(MISORT_E_INVALID, "alltoallv self count mismatch");
+        if (scnt[rank])
+            HIPCHK(hipMemcpyAsync((char*)recv + roff[rank], (const char*)send + soff[rank], (size_t)scnt[rank],
+                                  hipMemcpyDeviceToDevice, s));
+        NCCLCHK(ncclGroupStart());
+        for (int k = 1; k < nranks; ++k) {
+            const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
+            if (scnt[to]) NCCLCHK(ncclSend((const char*)send + soff[to], (size_t)scnt[to], ncclUint8, to, comm, s));
+            if (rcnt[from]) NCCLCHK(ncclRecv((char*)recv + roff[from], (size_t)rcnt[from], ncclUint8, from, comm, s));
+        }
+        NCCLCHK(ncclGroupEnd());
+        return MISORT_OK;
+    }
 };
 
 }  // namespace
@@ -205,6 +225,7 @@ struct misort_group {
         hipEvent_t ready = nullptr, done = nullptr;
         std::vector<uint64_t> posted, finished;
         std::vector<int64_t> vals;
+        std::vector<int64_t> a2a_off, a2a_cnt;  // alltoallv: this rank's send slices
     };
     std::vector<Slot> slots;
     uint64_t bar_count = 0, bar_gen = 0;
@@ -289,6 +310,32 @@ struct LocalTransport final : Transport {
         }
         // the peer has read my send buffer before this stream reuses it
         HIPCHK(hipStreamWaitEvent(s, pe.done, 0));
+        return MISORT_OK;
+    }
+    int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv, const int64_t* roff,
+                  const int64_t* rcnt, hipStream_t s) override {
+        auto& me = g->slots[rank];
+        HIPCHK(hipEventRecord(me.ready, s));
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            me.ptr = send;
+            me.a2a_off.assign(soff, soff + nranks);
+            me.a2a_cnt.assign(scnt, scnt + nranks);
+        }
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        for (int q = 0; q < nranks; ++q) {
+            const auto& pe = g->slots[q];
+            if (pe.a2a_cnt[rank] != rcnt[q])
+                return fail(MISORT_E_INVALID, "alltoallv size mismatch with rank %d (%lld vs %lld)", q,
+                            (long long)pe.a2a_cnt[rank], (long long)rcnt[q]);
+            if (!rcnt[q]) continue;
+            HIPCHK(hipStreamWaitEvent(s, pe.ready, 0));
+            HIPCHK(hipMemcpyAsync((char*)recv + roff[q], (const char*)pe.ptr + pe.a2a_off[rank], (size_t)rcnt[q],
+                                  hipMemcpyDeviceToDevice, s));
+        }
+        // every reader is done with every send buffer before anyone reuses it
+        HIPCHK(hipStreamSynchronize(s));
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
         return MISORT_OK;
     }
 };
@@ -555,6 +602,184 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
     return MISORT_OK;
 }
 
+// Sample sort (the reference's parallel_sample_{native,bitonic}_sort,
+// psort.cc:203-375, redesigned for RCCL over xGMI): local sort, regular
+// samples of every rank all-gathered, P-1 splitters taken as (key, rank,
+// position) tuples so that duplicate keys still split evenly, ONE all-to-all-v
+// in which every GPU pair uses its own link, a merge tree over the P received
+// runs, and a small second all-to-all-v that moves the keys into the
+// reference block layout (psort.cc:556-562).  The result is the globally
+// sorted sequence in the caller's block sizes.
+constexpr int kSamplesPerRank = 1024;
+
+int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc, int64_t max_size,
+                    hipStream_t s) {
+    if (!valid_dtype(dtype)) return fail(MISORT_E_INVALID, "bad dtype %d", dtype);
+    if (loc < 0 || max_size < loc) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld",
+                                               (long long)loc, (long long)max_size);
+    const int p = c->nranks, me = c->rank;
+    const size_t w = key_bytes(dtype);
+    const bool f64 = dtype == MISORT_F64;
+    int rc;
+    if ((rc = c->qa.ensure(std::max<size_t>(16, (size_t)loc * w)))) return rc;
+    if ((rc = do_local_sort(c, dtype, in, c->qa.p, loc, f64, s))) return rc;
+    if (p == 1) {
+        if (loc > 0) HIPCHK(hipMemcpyAsync(out, c->qa.p, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
+        if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, loc, s));
+        return MISORT_OK;
+    }
+    std::vector<int64_t> sizes;
+    if ((rc = c->tr->allgather_i64(&loc, 1, sizes, s))) return rc;
+    // regular samples a[j*S] of the sorted block, with their positions
+    const int M = kSamplesPerRank;
+    const int64_t S = std::max<int64_t>(1, (loc + M - 1) / M);
+    const int64_t cnt = loc > 0 ? (loc + S - 1) / S : 0;
+    if ((rc = c->samp_me.ensure((size_t)M * 8 + 16))) return rc;
+    std::vector<int64_t> mine(2 * (size_t)M, -1);
+    if (cnt > 0) {
+        hipError_t e = w == 4 ? misort::gather_samples<uint32_t>((const uint32_t*)c->qa.p, loc, S,
+                                                                 (uint32_t*)c->samp_me.p, cnt, s)
+                              : misort::gather_samples<uint64_t>((const uint64_t*)c->qa.p, loc, S,
+                                                                 (uint64_t*)c->samp_me.p, cnt, s);
+        if (e != hipSuccess) return fail(MISORT_E_HIP, "gather_samples: %s", hipGetErrorString(e));
+        std::vector<unsigned char> raw((size_t)cnt * w);
+        HIPCHK(hipMemcpyAsync(raw.data(), c->samp_me.p, raw.size(), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int64_t j = 0; j < cnt; ++j) {
+            uint64_t v = 0;
+            memcpy(&v, &raw[(size_t)j * w], w);
+            mine[2 * j] = (int64_t)v;
+            mine[2 * j + 1] = j * S;
+        }
+    }
+    std::vector<int64_t> all;
+    if ((rc = c->tr->allgather_i64(mine.data(), 2 * M, all, s))) return rc;
+    struct Tup {
+        uint64_t v;
+        int r;
+        int64_t pos;
+        bool operator<(const Tup& o) const {
+            return v != o.v ? v < o.v : r != o.r ? r < o.r : pos < o.pos;
+        }
+    };
+    std::vector<Tup> tup;
+    for (int r = 0; r < p; ++r)
+        for (int j = 0; j < M; ++j) {
+            const int64_t pos = all[((size_t)r * M + j) * 2 + 1];
+            if (pos >= 0) tup.push_back(Tup{(uint64_t)all[((size_t)r * M + j) * 2], r, pos});
+        }
+    std::sort(tup.begin(), tup.end());
+    // split points of this block for the P-1 splitters
+    std::vector<int64_t> split(p + 1, 0);
+    split[p] = loc;
+    const int ns = p - 1;
+    if (!tup.empty() && loc > 0) {
+        std::vector<Tup> sp(ns);
+        std::vector<unsigned char> vals((size_t)ns * w);
+        for (int j = 1; j < p; ++j) {
+            sp[j - 1] = tup[(size_t)j * tup.size() / p];
+            memcpy(&vals[(size_t)(j - 1) * w], &sp[j - 1].v, w);
+        }
+        if ((rc = c->samp_peer.ensure(vals.size() + 16))) return rc;
+        if ((rc = c->qcnt.ensure((size_t)ns * 16 + 64))) return rc;
+        int64_t* dlb = (int64_t*)c->qcnt.p;
+        int64_t* dub = dlb + ns;
+        HIPCHK(hipMemcpyAsync(c->samp_peer.p, vals.data(), vals.size(), hipMemcpyHostToDevice, s));
+        hipError_t e = w == 4 ? misort::bounds<uint32_t>((const uint32_t*)c->qa.p, loc, (const uint32_t*)c->samp_peer.p,
+                                                         ns, dlb, dub, s)
+                              : misort::bounds<uint64_t>((const uint64_t*)c->qa.p, loc, (const uint64_t*)c->samp_peer.p,
+                                                         ns, dlb, dub, s);
+        if (e != hipSuccess) return fail(MISORT_E_HIP, "bounds: %s", hipGetErrorString(e));
+        std::vector<int64_t> lbub(2 * (size_t)ns);
+        HIPCHK(hipMemcpyAsync(lbub.data(), dlb, lbub.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int j = 1; j < p; ++j) {
+            const Tup& t = sp[j - 1];
+            // keys of this rank below the tuple (key, rank, position) in (key, rank, position) order
+            int64_t x = me < t.r ? lbub[ns + j - 1] : me > t.r ? lbub[j - 1] : t.pos;
+            split[j] = std::max(split[j - 1], std::min(x, loc));
+        }
+    } else if (loc > 0) {
+        for (int j = 1; j < p; ++j) split[j] = 0;  // no samples anywhere: everything to the last rank
+    }
+    std::vector<int64_t> scnt(p), soff(p), rcnt(p), roff(p), kc(p);
+    for (int q = 0; q < p; ++q) {
+        kc[q] = split[q + 1] - split[q];
+        soff[q] = split[q] * (int64_t)w;
+        scnt[q] = kc[q] * (int64_t)w;
+    }
+    std::vector<int64_t> mat;
+    if ((rc = c->tr->allgather_i64(kc.data(), p, mat, s))) return rc;
+    int64_t nrecv = 0;
+    for (int q = 0; q < p; ++q) {
+        rcnt[q] = mat[(size_t)q * p + me] * (int64_t)w;
+        roff[q] = nrecv * (int64_t)w;
+        nrecv += mat[(size_t)q * p + me];
+    }
+    if ((rc = c->recv.ensure(std::max<size_t>(16, (size_t)nrecv * w)))) return rc;
+    if ((rc = c->qb.ensure(std::max<size_t>(16, (size_t)nrecv * w)))) return rc;
+    if ((rc = c->tr->alltoallv(c->qa.p, soff.data(), scnt.data(), c->recv.p, roff.data(), rcnt.data(), s)))
+        return rc;
+    c->xchg_stages += 1;
+    c->xchg_bytes += (int64_t)(loc * w - scnt[me] + nrecv * w - rcnt[me]);
+    // merge tree over the P runs (adjacent pairs keep their place, buffers alternate)
+    std::vector<int64_t> ro(p), rn(p);
+    for (int q = 0; q < p; ++q) {
+        ro[q] = roff[q] / (int64_t)w;
+        rn[q] = rcnt[q] / (int64_t)w;
+    }
+    char* src = (char*)c->recv.p;
+    char* dst = (char*)c->qb.p;
+    if ((rc = c->scratch.ensure((size_t)((nrecv + 2047) / 2048 + p + 2) * sizeof(int64_t)))) return rc;
+    while (ro.size() > 1) {
+        std::vector<int64_t> no, nn;
+        for (size_t i = 0; i < ro.size(); i += 2) {
+            if (i + 1 == ro.size()) {
+                if (rn[i]) HIPCHK(hipMemcpyAsync(dst + ro[i] * w, src + ro[i] * w, (size_t)rn[i] * w,
+                                                 hipMemcpyDeviceToDevice, s));
+                no.push_back(ro[i]);
+                nn.push_back(rn[i]);
+                continue;
+            }
+            hipError_t e = w == 4
+                ? misort::merge_full<uint32_t>((const uint32_t*)(src + ro[i] * w), rn[i],
+                                               (const uint32_t*)(src + ro[i + 1] * w), rn[i + 1],
+                                               (uint32_t*)(dst + ro[i] * w), (int64_t*)c->scratch.p, s, hook(c))
+                : misort::merge_full<uint64_t>((const uint64_t*)(src + ro[i] * w), rn[i],
+                                               (const uint64_t*)(src + ro[i + 1] * w), rn[i + 1],
+                                               (uint64_t*)(dst + ro[i] * w), (int64_t*)c->scratch.p, s, hook(c));
+            if (e != hipSuccess) return fail(MISORT_E_HIP, "merge: %s", hipGetErrorString(e));
+            no.push_back(ro[i]);
+            nn.push_back(rn[i] + rn[i + 1]);
+        }
+        ro.swap(no);
+        rn.swap(nn);
+        std::swap(src, dst);
+    }
+    // the reference block layout: keys at global ranks [T_q, T_q + sizes[q]) go to rank q
+    std::vector<int64_t> have;
+    if ((rc = c->tr->allgather_i64(&nrecv, 1, have, s))) return rc;
+    int64_t A = 0, Tme = 0;
+    for (int q = 0; q < me; ++q) {
+        A += have[q];
+        Tme += sizes[q];
+    }
+    int64_t Tq = 0, Aq = 0;
+    for (int q = 0; q < p; ++q) {
+        const int64_t s0 = std::max(A, Tq), s1 = std::min(A + nrecv, Tq + sizes[q]);
+        soff[q] = (s1 > s0 ? s0 - A : 0) * (int64_t)w;
+        scnt[q] = (s1 > s0 ? s1 - s0 : 0) * (int64_t)w;
+        const int64_t r0 = std::max(Aq, Tme), r1 = std::min(Aq + have[q], Tme + loc);
+        roff[q] = (r1 > r0 ? r0 - Tme : 0) * (int64_t)w;
+        rcnt[q] = (r1 > r0 ? r1 - r0 : 0) * (int64_t)w;
+        Tq += sizes[q];
+        Aq += have[q];
+    }
+    if ((rc = c->tr->alltoallv(src, soff.data(), scnt.data(), out, roff.data(), rcnt.data(), s))) return rc;
+    if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, loc, s));
+    return MISORT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -762,6 +987,15 @@ int misort_parallel_quick_sort(misort_ctx* c, int dtype, const void* in, int64_t
     if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     if ((loc > 0 && !in) || (out_capacity > 0 && !out)) return fail(MISORT_E_INVALID, "null buffer");
     return parallel_quick(c, dtype, in, loc, out, out_capacity, out_size, pick(c, stream));
+}
+
+int misort_parallel_sample_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
+                                int64_t max_size, void* stream) {
+    if (!c) return fail(MISORT_E_INVALID, "null ctx");
+    if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
+    if (loc > 0 && (!in || !out)) return fail(MISORT_E_INVALID, "null buffer");
+    if (in == out && loc > 0) return fail(MISORT_E_INVALID, "sample sort is out of place (d_in != d_out)");
+    return parallel_sample(c, dtype, in, out, loc, max_size, pick(c, stream));
 }
 
 int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc, const void* recv,

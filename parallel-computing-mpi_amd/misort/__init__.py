@@ -77,6 +77,7 @@ def lib():
         "misort_local_sort": ([vp, i32, vp, vp, i64, vp], i32),
         "misort_merge_split": ([vp, i32, vp, i64, vp, i64, vp, i32, vp], i32),
         "misort_parallel_quick_sort": ([vp, i32, vp, i64, vp, i64, ctypes.POINTER(i64), vp], i32),
+        "misort_parallel_sample_sort": ([vp, i32, vp, vp, i64, i64, vp], i32),
         "misort_check_sort": ([vp, i32, vp, i64, ctypes.POINTER(i64), vp], i32),
         "misort_sort_host": ([vp, i32, vp, vp, i64, i64], i32),
         "misort_fill_splitmix": ([vp, i32, vp, i64, ctypes.c_uint64, i64, vp], i32),
@@ -290,6 +291,18 @@ class Context:
         _check(lib().misort_parallel_quick_sort(self._h, _dtype_of(buffer), _ptr(buffer), loc, _ptr(out),
                                                 out.numel(), ctypes.byref(n), self._stream(stream)))
         return out, int(n.value)
+
+    def parallel_sample_sort(self, buffer, loc_buf_size=None, max_size=None, out=None, stream=None):
+        """psort.cc:203-375 redesigned (RCCL all-to-all).  Same contract as
+        parallel_bitonic_sort: the globally sorted keys in the reference block
+        layout, out of place (``out`` defaults to a new tensor)."""
+        import torch
+        loc = buffer.numel() if loc_buf_size is None else int(loc_buf_size)
+        mx = loc if max_size is None else int(max_size)
+        out = torch.empty_like(buffer) if out is None else out
+        _check(lib().misort_parallel_sample_sort(self._h, _dtype_of(buffer), _ptr(buffer), _ptr(out), loc, mx,
+                                                 self._stream(stream)))
+        return out
 
     def local_sort(self, inp, out=None, n=None, stream=None):
         """psort.cc:175 (std::sort of the local block) on the GPU."""
