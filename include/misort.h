@@ -173,6 +173,12 @@ int misort_fill_splitmix(misort_ctx* ctx, int dtype, void* d_out, int64_t n, uin
                          int64_t g0, void* stream);
 
 int misort_set_full_exchange(misort_ctx* ctx, int on);
+
+/* Relay each compare-split exchange through the other GPUs (P > 2; default on,
+ * env MISORT_RELAY=0 turns it off): every message is cut into P parts, 2 go
+ * over the pair's own xGMI link, P-2 take two hops through the other GPUs, so
+ * all P-1 links of every GPU carry the stage.  Bytes delivered are identical. */
+int misort_set_relay(misort_ctx* ctx, int on);
 /* Host logic of the bracketed exchange (pure functions, no GPU):
  * samples of a sorted block of n keys are keys[min(c*S, n-1)], c = 0..count-1,
  * S = misort_sample_stride(n), count = misort_sample_count(n).

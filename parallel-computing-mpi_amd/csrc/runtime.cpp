@@ -160,6 +160,16 @@ struct Transport {
     // device buffers; both sides know both byte counts
     virtual int sendrecv(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, int peer,
                          hipStream_t s) = 0;
+    // one group of point-to-point transfers (no self transfers; at most one
+    // message per (sender, receiver) pair; both sides post matching sizes)
+    struct Op {
+        int peer;
+        bool send;
+        const void* sptr;
+        void* rptr;
+        size_t bytes;
+    };
+    virtual int group_p2p(const std::vector<Op>& ops, hipStream_t s) = 0;
     // all-to-all-v on device buffers: to rank q go send[soff[q], +scnt[q]) bytes,
     // from rank q come recv[roff[q], +rcnt[q]); every rank knows its own counts
     virtual int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv,
@@ -188,6 +198,16 @@ struct RcclTransport final : Transport {
         NCCLCHK(ncclGroupStart());
         if (sb) NCCLCHK(ncclSend(send, sb, ncclUint8, peer, comm, s));
         if (rb) NCCLCHK(ncclRecv(recv, rb, ncclUint8, peer, comm, s));
+        NCCLCHK(ncclGroupEnd());
+        return MISORT_OK;
+    }
+    int group_p2p(const std::vector<Op>& ops, hipStream_t s) override {
+        NCCLCHK(ncclGroupStart());
+        for (const Op& o : ops) {
+            if (!o.bytes) continue;
+            if (o.send) NCCLCHK(ncclSend(o.sptr, o.bytes, ncclUint8, o.peer, comm, s));
+            else NCCLCHK(ncclRecv(o.rptr, o.bytes, ncclUint8, o.peer, comm, s));
+        }
         NCCLCHK(ncclGroupEnd());
         return MISORT_OK;
     }
@@ -226,6 +246,7 @@ struct misort_group {
         std::vector<uint64_t> posted, finished;
         std::vector<int64_t> vals;
         std::vector<int64_t> a2a_off, a2a_cnt;  // alltoallv: this rank's send slices
+        std::vector<std::pair<const void*, size_t>> p2p_send;  // group_p2p: message to each rank
     };
     std::vector<Slot> slots;
     uint64_t bar_count = 0, bar_gen = 0;
@@ -312,6 +333,30 @@ struct LocalTransport final : Transport {
         HIPCHK(hipStreamWaitEvent(s, pe.done, 0));
         return MISORT_OK;
     }
+    int group_p2p(const std::vector<Op>& ops, hipStream_t s) override {
+        auto& me = g->slots[rank];
+        HIPCHK(hipEventRecord(me.ready, s));
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            me.p2p_send.assign(nranks, {nullptr, 0});
+            for (const Op& o : ops)
+                if (o.send) me.p2p_send[o.peer] = {o.sptr, o.bytes};
+        }
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        for (const Op& o : ops) {
+            if (o.send) continue;
+            const auto& pe = g->slots[o.peer];
+            if (pe.p2p_send[rank].second != o.bytes)
+                return fail(MISORT_E_INVALID, "group_p2p size mismatch from rank %d (%zu vs %zu)", o.peer,
+                            pe.p2p_send[rank].second, o.bytes);
+            if (!o.bytes) continue;
+            HIPCHK(hipStreamWaitEvent(s, pe.ready, 0));
+            HIPCHK(hipMemcpyAsync(o.rptr, pe.p2p_send[rank].first, o.bytes, hipMemcpyDeviceToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        return MISORT_OK;
+    }
     int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv, const int64_t* roff,
                   const int64_t* rcnt, hipStream_t s) override {
         auto& me = g->slots[rank];
@@ -354,6 +399,9 @@ struct misort_ctx {
     Profiler prof;
     int64_t xchg_bytes = 0, xchg_stages = 0, xchg_full_bytes = 0;
     bool full_exchange = getenv("MISORT_FULL_EXCHANGE") != nullptr;
+    // relay compare-split exchanges through the other GPUs (P > 2): MISORT_RELAY=0 disables
+    bool relay = !getenv("MISORT_RELAY") || atoi(getenv("MISORT_RELAY")) != 0;
+    DevBuf relay_buf;
     ~misort_ctx() { delete tr; }
 };
 
@@ -418,6 +466,69 @@ int64_t corank_lower(const std::vector<T>& sa, int64_t na, const std::vector<T>&
         else hi = mid;
     }
     return lo;
+}
+
+// Pair exchange of one hypercube stage (partner = rank ^ 2^bit) spread over
+// every xGMI link.  A stage pairs the P GPUs, so a plain send/recv drives one
+// of each GPU's P-1 links.  Here each message is cut into P parts: parts 0 and
+// 1 go straight to the partner (one per round), part 2+j goes through the j-th
+// other GPU, which receives it in round 1 and forwards it in round 2.  Every
+// directed link carries one part per round, so a stage moves in 2/P of the
+// direct time (4x less at P = 8).  All ranks take part, including those whose
+// own message is empty, because they relay for the others.
+int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sbytes, void* rbuf, size_t rbytes,
+                   hipStream_t s) {
+    const int P = c->nranks, me = c->rank, pm = me ^ (1 << bit);
+    int rc;
+    std::vector<int64_t> m;  // keys each rank sends to its partner
+    const int64_t mine = (int64_t)(sbytes / w);
+    if ((rc = c->tr->allgather_i64(&mine, 1, m, s))) return rc;
+    if ((size_t)m[pm] * w != rbytes) return fail(MISORT_E_INVALID, "relay: partner size mismatch");
+    auto bnd = [&](int x, int i) { return (int64_t)((__int128)i * m[x] / P); };
+    auto rel = [&](int x) {  // relays of x's pair, ascending
+        std::vector<int> r;
+        for (int y = 0; y < P; ++y)
+            if (y != x && y != (x ^ (1 << bit))) r.push_back(y);
+        return r;
+    };
+    auto idx_in = [&](int x, int y) {
+        const std::vector<int> r = rel(x);
+        return (int)(std::find(r.begin(), r.end(), y) - r.begin());
+    };
+    // staging for the parts this rank relays: x's part 2 + idx_in(x, me)
+    std::vector<int64_t> soff(P, 0), scnt(P, 0);
+    int64_t tot = 0;
+    for (int x = 0; x < P; ++x) {
+        if (x == me || x == pm) continue;
+        const int j = idx_in(x, me);
+        soff[x] = tot;
+        scnt[x] = bnd(x, 3 + j) - bnd(x, 2 + j);
+        tot += scnt[x];
+    }
+    if ((rc = c->relay_buf.ensure(std::max<size_t>(16, (size_t)tot * w)))) return rc;
+    char* stg = (char*)c->relay_buf.p;
+    const char* sb = (const char*)sbuf;
+    char* rb = (char*)rbuf;
+    const std::vector<int> mine_rel = rel(me);
+    std::vector<Transport::Op> r1, r2;
+    r1.push_back({pm, true, sb + bnd(me, 0) * w, nullptr, (size_t)(bnd(me, 1) - bnd(me, 0)) * w});
+    r1.push_back({pm, false, nullptr, rb + bnd(pm, 0) * w, (size_t)(bnd(pm, 1) - bnd(pm, 0)) * w});
+    r2.push_back({pm, true, sb + bnd(me, 1) * w, nullptr, (size_t)(bnd(me, 2) - bnd(me, 1)) * w});
+    r2.push_back({pm, false, nullptr, rb + bnd(pm, 1) * w, (size_t)(bnd(pm, 2) - bnd(pm, 1)) * w});
+    for (size_t j = 0; j < mine_rel.size(); ++j) {
+        const int y = mine_rel[j];
+        r1.push_back({y, true, sb + bnd(me, 2 + (int)j) * w, nullptr,
+                      (size_t)(bnd(me, 3 + (int)j) - bnd(me, 2 + (int)j)) * w});
+        r2.push_back({y, false, nullptr, rb + bnd(pm, 2 + (int)j) * w,
+                      (size_t)(bnd(pm, 3 + (int)j) - bnd(pm, 2 + (int)j)) * w});
+    }
+    for (int x = 0; x < P; ++x) {
+        if (x == me || x == pm) continue;
+        r1.push_back({x, false, nullptr, stg + soff[x] * w, (size_t)scnt[x] * w});
+        r2.push_back({x ^ (1 << bit), true, stg + soff[x] * w, nullptr, (size_t)scnt[x] * w});
+    }
+    if ((rc = c->tr->group_p2p(r1, s))) return rc;
+    return c->tr->group_p2p(r2, s);
 }
 
 int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
@@ -491,7 +602,11 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         }
         c->xchg_stages += 1;
         c->xchg_full_bytes += (int64_t)((loc + nq) * w);
-        if (k == 0) continue;  // no key crosses: both blocks stay as they are
+        const bool relayed = c->relay && p > 2;
+        if (k == 0) {  // no key crosses: both blocks stay as they are
+            if (relayed && (rc = relay_exchange(c, w, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
+            continue;
+        }
         // A sends its top k = A[na-k, na); B sends its bottom k = B[0, k)
         const void* sbuf;
         size_t sbytes, rbytes;
@@ -506,7 +621,9 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             sbytes = rbytes = (size_t)k * w;
             nrecv = k;
         }
-        if ((rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s))) return rc;
+        if (relayed) rc = relay_exchange(c, w, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
+        else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
+        if (rc) return rc;
         c->xchg_bytes += (int64_t)(sbytes + rbytes);
         if ((rc = do_merge_split(c, dtype, cur, loc, c->recv.p, nrecv, other, keep[st], s))) return rc;
         std::swap(cur, other);
@@ -916,6 +1033,12 @@ int64_t misort_exchange_count(int dtype, const void* samples_min, int64_t n_min,
         ilo = corank_lower(a, n_min, b, n_max);
     }
     return n_min - ilo;
+}
+
+int misort_set_relay(misort_ctx* c, int on) {
+    if (!c) return fail(MISORT_E_INVALID, "null ctx");
+    c->relay = on != 0;
+    return MISORT_OK;
 }
 
 int misort_set_full_exchange(misort_ctx* c, int on) {

@@ -90,6 +90,7 @@ def lib():
         "misort_group_destroy": ([vp], i32),
         "misort_comm_init_group": ([vp, vp, i32], i32),
         "misort_set_full_exchange": ([vp, i32], i32),
+        "misort_set_relay": ([vp, i32], i32),
         "misort_sample_stride": ([i64], i64),
         "misort_sample_count": ([i64], i64),
         "misort_exchange_count": ([i32, vp, i64, vp, i64], i64),
@@ -356,6 +357,10 @@ class Context:
 
     def set_full_exchange(self, on=True):
         _check(lib().misort_set_full_exchange(self._h, int(on)))
+
+    def set_relay(self, on=True):
+        """Spread compare-split exchanges over every xGMI link (P > 2)."""
+        _check(lib().misort_set_relay(self._h, int(on)))
 
     def exchange_stats(self):
         """(stages, bytes moved, bytes a whole-block exchange would move); resets."""

@@ -56,7 +56,7 @@ def to_host(t, dtype):
     return t.cpu().numpy()
 
 
-def group_sort(x, p, full_exchange=False, out_of_place=False):
+def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True):
     """Each rank sorts its reference-layout block; returns (concatenated
     result, check_sort count of every rank, exchange stats of every rank)."""
     sizes = misort.block_sizes(x.size, p)
@@ -66,6 +66,7 @@ def group_sort(x, p, full_exchange=False, out_of_place=False):
 
     def rank_fn(r, ctx):
         ctx.set_full_exchange(full_exchange)
+        ctx.set_relay(relay)
         buf = to_dev(np.concatenate([blocks[r], np.zeros(max_size - sizes[r], x.dtype)]))
         out = torch.empty_like(buf) if out_of_place else None
         torch.cuda.synchronize()
@@ -121,6 +122,20 @@ def test_u32_partial_vs_full_exchange(p, n):
     moved = sum(s[1] for s in st1)
     assert moved < sum(s[1] for s in st2)  # the bracket saves bytes
     assert sum(s[1] for s in st2) == sum(s[2] for s in st2)
+
+
+@pytest.mark.parametrize("p", [4, 8])
+@pytest.mark.parametrize("full", [False, True])
+def test_relayed_exchange_equals_direct(p, full):
+    # the xGMI relay (messages cut into P parts, P-2 of them two hops through
+    # the other GPUs) delivers the same bytes as the direct pair exchange,
+    # including asymmetric whole-block messages (N % P != 0) and k = 0 stages
+    x = O.splitmix(0x5EED0009 + p, (1 << 21) + 3, np.uint32)
+    y1, e1, st1 = group_sort(x, p, full_exchange=full, relay=True)
+    y2, e2, st2 = group_sort(x, p, full_exchange=full, relay=False)
+    np.testing.assert_array_equal(y1, y2)
+    np.testing.assert_array_equal(y1, O.parallel_bitonic_sort(x, p))
+    assert e1 == e2 and st1 == st2
 
 
 @pytest.mark.parametrize("p", [2, 4, 8])
