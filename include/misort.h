@@ -52,7 +52,8 @@ enum misort_kernel_kind {
     MISORT_K_GLOBAL = 1,      /* fused large-stride HBM pass             */
     MISORT_K_TILE_MERGE = 2,  /* in-tile strides of one merge level      */
     MISORT_K_MERGE_SPLIT = 3, /* device compare-split (psort.cc:116-164) */
-    MISORT_K_OTHER = 4
+    MISORT_K_OTHER = 4,
+    MISORT_K_SPAN = 5         /* tail of one level + head of the next    */
 };
 
 typedef struct misort_ctx misort_ctx;
@@ -205,6 +206,12 @@ int misort_profile_read(misort_ctx* ctx, int kind, int64_t* launches, double* to
 
 /* log2 of the LDS tile (keys) used for a key width of 4 or 8 bytes. */
 int misort_tile_log2(int key_bytes);
+
+/* The HBM pass plan of a local sort of n keys (key_bytes 4 or 8), for tools
+ * and tests: writes up to max_passes entries of 4 ints (kind as
+ * misort_kernel_kind, hi, R, flip) and returns the number of passes (or a
+ * negative status).  Host-only; no device is touched. */
+int misort_plan(int64_t n, int key_bytes, int* passes, int max_passes);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,11 @@
 //                    is 2^R rows at the stride distance times 2^(LT-R)
 //                    consecutive keys, so every row segment is a coalesced
 //                    >= 128 B run;
-//   k_stream<MERGE>  the strides < 2^LT of one level, in an LDS tile.
+//   k_stream<MERGE>  the strides < 2^LT of one level, in an LDS tile;
+//   k_stream<SPAN>   the last LT-R strides of level m (2^(LT-R-1)..1) AND the
+//                    first R strides of level m+1 (its flip, then
+//                    2^(m-1)..2^(m-R+1)) in one ROWS-shaped tile, so the pass
+//                    boundary need not fall on a level boundary (see plan()).
 // All of them share one tile engine (one-shot or persistent + prefetching).
 //
 // A pass over n keys moves 2 * n * sizeof(K) algorithmic HBM bytes.
@@ -44,9 +48,14 @@ namespace misort {
 //                          flight (default 3); the others launch one workgroup
 //                          per tile;
 //   MISORT_PINGPONG        1 (default): passes alternate between the output and
-//                          a scratch buffer (copy-shaped HBM traffic); 0: in place.
+//                          a scratch buffer (copy-shaped HBM traffic); 0: in place;
+//   MISORT_SPAN            1 (default): plan passes across level boundaries with
+//                          SPAN passes (fewest passes); 0: one MERGE per level;
+//   MISORT_ROW_BYTES_LOG2  shortest row run a ROWS/SPAN tile may use (default 8:
+//                          256 B; 7 allows 128-B rows).
 struct PlanKnobs {
-    int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3, grid_mult = 1, pingpong = 1;
+    int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
+    int span = 1, row_bytes_log2 = 8;
     PlanKnobs();
 };
 const PlanKnobs& plan_knobs();
@@ -150,7 +159,10 @@ __device__ __forceinline__ void store_vec(K* __restrict__ p, int64_t i0, int64_t
 // LDS layout: key v at word v + v/32.  The padding keeps every phase's
 // 32-lane accesses on distinct banks, and since v + v/32 is additive over
 // disjoint bit fields every access is one base VGPR plus an immediate offset.
-enum TileMode : int { TM_SORT = 0, TM_MERGE = 1, TM_ROWS = 2 };
+enum TileMode : int { TM_SORT = 0, TM_MERGE = 1, TM_ROWS = 2, TM_SPAN = 3 };
+
+// ROWS and SPAN tiles are row-shaped; SORT and MERGE tiles are contiguous.
+__host__ __device__ constexpr bool rowsy(int mode) { return mode == TM_ROWS || mode == TM_SPAN; }
 
 struct TileMap {
     int64_t ntiles;  // real tiles (a prefix of the tile list)
@@ -172,7 +184,7 @@ struct TileGeo {
 
 template <int LT, int MODE>
 __device__ __forceinline__ int64_t tile_index(const TileMap& m, int64_t tile, int e) {
-    if constexpr (MODE != TM_ROWS) {
+    if constexpr (!rowsy(MODE)) {
         return (tile << LT) + e;
     } else {
         const int R = LT - m.logB;
@@ -189,7 +201,7 @@ __device__ __forceinline__ int64_t tile_index(const TileMap& m, int64_t tile, in
 // Every key of the tile lies below n (then no per-element bounds checks).
 template <int LT, int MODE>
 __device__ __forceinline__ bool tile_full(const TileMap& m, int64_t tile, int64_t n) {
-    if constexpr (MODE != TM_ROWS) {
+    if constexpr (!rowsy(MODE)) {
         return ((tile + 1) << LT) <= n;
     } else {
         return (((tile >> (m.lo - m.logB)) + 1) << (m.hi + 1)) <= n;
@@ -369,6 +381,12 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
                 sort_levels<K, 6, LT>(s, t);
             } else if constexpr (MODE == TM_MERGE) {
                 lds_range<K, LT - G::KB - 1, G::VB, false>(s, t);
+            } else if constexpr (MODE == TM_SPAN) {
+                // tail of level m on the row-run bits, then level m+1's flip
+                // (v <-> ~v: the tile's mirrored rows make it the global
+                // mirror) and its half-cleaners on the row bits
+                lds_range<K, LT - R - 1, 0, false>(s, t);
+                lds_range<K, LT - 1, LT - R, true>(s, t);
             } else {
                 lds_range<K, LT - G::KB - 1, LT - R, false>(s, t);
             }
@@ -434,16 +452,20 @@ void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t
     else k_stream<K, LT, MODE, R, FLIP, ORD, false><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
 }
 
-template <typename K, int LT, int R>
+template <typename K, int LT, int MODE, int R>
 void launch_rows_r(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
     if constexpr (R <= LT - 5) {
-        if (m.flip) launch_stream<K, LT, TM_ROWS, R, true, false>(in, out, n, m, s);
-        else launch_stream<K, LT, TM_ROWS, R, false, false>(in, out, n, m, s);
+        if constexpr (MODE == TM_SPAN) launch_stream<K, LT, MODE, R, true, false>(in, out, n, m, s);
+        else if (m.flip) launch_stream<K, LT, MODE, R, true, false>(in, out, n, m, s);
+        else launch_stream<K, LT, MODE, R, false, false>(in, out, n, m, s);
     }
 }
 
-// One ROWS pass: strides 2^hi .. 2^(hi-R+1) of a level over n (virtual) keys.
-template <typename K, int LT>
+// One ROWS pass (strides 2^hi .. 2^(hi-R+1) of a level) or SPAN pass (the
+// strides 2^(LT-R-1)..1 of level hi, then level hi+1's flip and strides
+// 2^(hi-1)..2^(hi-R+1)) over n (virtual) keys.  Both use the tile of 2^R rows
+// at stride 2^(hi-R+1) times 2^(LT-R) consecutive keys.
+template <typename K, int LT, int MODE>
 void launch_rows(const K* in, K* out, int64_t n, int hi, int R, bool flip, hipStream_t s) {
     TileMap m{};
     m.lo = hi - R + 1;
@@ -457,30 +479,30 @@ void launch_rows(const K* in, K* out, int64_t n, int hi, int R, bool flip, hipSt
     if (part > per_seg) part = per_seg;
     m.ntiles = full_segs * per_seg + part;
     switch (R) {
-        case 1: launch_rows_r<K, LT, 1>(in, out, n, m, s); break;
-        case 2: launch_rows_r<K, LT, 2>(in, out, n, m, s); break;
-        case 3: launch_rows_r<K, LT, 3>(in, out, n, m, s); break;
-        case 4: launch_rows_r<K, LT, 4>(in, out, n, m, s); break;
-        case 5: launch_rows_r<K, LT, 5>(in, out, n, m, s); break;
-        case 6: launch_rows_r<K, LT, 6>(in, out, n, m, s); break;
-        case 7: launch_rows_r<K, LT, 7>(in, out, n, m, s); break;
-        case 8: launch_rows_r<K, LT, 8>(in, out, n, m, s); break;
-        case 9: launch_rows_r<K, LT, 9>(in, out, n, m, s); break;
-        default: launch_rows_r<K, LT, 10>(in, out, n, m, s); break;
+        case 1: launch_rows_r<K, LT, MODE, 1>(in, out, n, m, s); break;
+        case 2: launch_rows_r<K, LT, MODE, 2>(in, out, n, m, s); break;
+        case 3: launch_rows_r<K, LT, MODE, 3>(in, out, n, m, s); break;
+        case 4: launch_rows_r<K, LT, MODE, 4>(in, out, n, m, s); break;
+        case 5: launch_rows_r<K, LT, MODE, 5>(in, out, n, m, s); break;
+        case 6: launch_rows_r<K, LT, MODE, 6>(in, out, n, m, s); break;
+        case 7: launch_rows_r<K, LT, MODE, 7>(in, out, n, m, s); break;
+        case 8: launch_rows_r<K, LT, MODE, 8>(in, out, n, m, s); break;
+        case 9: launch_rows_r<K, LT, MODE, 9>(in, out, n, m, s); break;
+        default: launch_rows_r<K, LT, MODE, 10>(in, out, n, m, s); break;
     }
 }
 
 // One HBM pass of the plan.
 struct Pass {
-    Kind kind;  // KIND_TILE_SORT, KIND_GLOBAL (ROWS), KIND_TILE_MERGE
-    int hi, R;
+    Kind kind;  // KIND_TILE_SORT, KIND_GLOBAL (ROWS), KIND_SPAN, KIND_TILE_MERGE
+    int hi, R;  // ROWS: strides 2^hi..2^(hi-R+1); SPAN: level hi+1's head of R strides
     bool flip;
 };
 
-// Pass plan for 2^k (virtual) keys: one SORT pass (levels 1..LT of each 2^LT
-// tile), then per level m > LT the strides 2^(m-1)..2^LT in near-equal ROWS
-// passes of <= rmax strides each, and one MERGE pass for the strides < 2^LT.
-inline std::vector<Pass> plan(int k, int LT, int rmax) {
+// Level-by-level plan (MISORT_SPAN=0): one SORT pass (levels 1..LT of each
+// 2^LT tile), then per level m > LT the strides 2^(m-1)..2^LT in near-equal
+// ROWS passes of <= rmax strides each, and one MERGE pass for the strides < 2^LT.
+inline std::vector<Pass> plan_levels(int k, int LT, int rmax) {
     std::vector<Pass> ps;
     ps.push_back(Pass{KIND_TILE_SORT, LT - 1, 0, false});
     for (int m = LT + 1; m <= k; ++m) {
@@ -497,13 +519,81 @@ inline std::vector<Pass> plan(int k, int LT, int rmax) {
     return ps;
 }
 
+// Cheapest plan (default).  After the SORT pass, the stages of levels LT+1..k
+// form one sequence of (level m, stride bit b) for b = m-1..0.  A pass takes a
+// consecutive run of it whose bits fit one LT-bit tile:
+//   ROWS  bits hi..hi-R+1 of one level (flip iff hi = m-1), R <= rmax, whose
+//         tile keeps >= 2^cmin consecutive keys per row (coalescing);
+//   MERGE bits LT-1..0 of one level;
+//   SPAN  bits LT-R-1..0 of level m, then bits m..m-R+1 of level m+1 (the
+//         flip first): a ROWS tile of R row bits whose 2^(LT-R)-key rows hold
+//         the tail's bits.
+// Dynamic programming over the sequence minimises the modelled time: every
+// pass costs one HBM sweep, ROWS tiles with the shortest (2^cmin-key) rows and
+// SPAN passes (more LDS phases) a little more.  For 2^30 u32 keys this is
+// 1 + 29 passes instead of the level-by-level plan's 1 + 35.
+inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin) {
+    struct St { int m, b; };
+    std::vector<St> seq;
+    for (int m = LT + 1; m <= k; ++m)
+        for (int b = m - 1; b >= 0; --b) seq.push_back(St{m, b});
+    const int N = (int)seq.size();
+    const double INF = 1e30;
+    std::vector<double> best(N + 1, INF);
+    std::vector<Pass> how(N + 1);
+    std::vector<int> nxt(N + 1, N);
+    best[N] = 0;
+    for (int p = N - 1; p >= 0; --p) {
+        const int m = seq[p].m, b = seq[p].b;
+        auto take = [&](int q, double c, Pass ps) {
+            if (q <= N && best[q] + c < best[p]) {
+                best[p] = best[q] + c;
+                how[p] = ps;
+                nxt[p] = q;
+            }
+        };
+        if (b >= LT) {
+            for (int R = 1; R <= rmax && LT - R >= cmin; ++R) {
+                const int lo = b - R + 1;
+                if (lo < LT - R) break;
+                take(p + R, 1.0 + (LT - R == cmin ? 0.05 : 0.0), Pass{KIND_GLOBAL, b, R, b == m - 1});
+            }
+        } else if (b == LT - 1) {
+            take(p + LT, 0.97, Pass{KIND_TILE_MERGE, LT - 1, 0, false});
+        }
+        if (b < LT && m < k) {
+            const int R = LT - (b + 1);
+            if (R >= 1 && R <= rmax && LT - R >= cmin)
+                take(p + (b + 1) + R, 1.02, Pass{KIND_SPAN, m, R, true});
+        }
+    }
+    std::vector<Pass> ps;
+    ps.push_back(Pass{KIND_TILE_SORT, LT - 1, 0, false});
+    if (N > 0 && best[0] >= INF) return plan_levels(k, LT, rmax);
+    for (int p = 0; p < N; p = nxt[p]) ps.push_back(how[p]);
+    return ps;
+}
+
+inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span) {
+    return span ? plan_span(k, LT, rmax, cmin) : plan_levels(k, LT, rmax);
+}
+
+// The plan local_sort_lt runs for n keys (shared with plan_passes()).
+template <typename K, int LT, int LTR>
+std::vector<Pass> plan_for(int64_t n) {
+    const PlanKnobs& kn = plan_knobs();
+    const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
+    int cmin = kn.row_bytes_log2 - (sizeof(K) == 4 ? 2 : 3);
+    if (cmin < 5) cmin = 5;
+    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR);
+}
+
 // LT: SORT/MERGE tile; LTR: ROWS tile.
 template <typename K, int LT, int LTR>
 hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                          LaunchHook* hook) {
     const PlanKnobs& kn = plan_knobs();
-    const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
-    const std::vector<Pass> ps = plan(ceil_log2(n), LT, rmax);
+    const std::vector<Pass> ps = plan_for<K, LT, LTR>(n);
     const int np = (int)ps.size();
     const bool pp = kn.pingpong && scratch != nullptr && scratch != out && scratch != in;
     const double bytes = 2.0 * (double)n * sizeof(K);
@@ -523,7 +613,9 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
                 launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
             }
         } else if (p.kind == KIND_GLOBAL) {
-            launch_rows<K, LTR>(src, dst, n, p.hi, p.R, p.flip, s);
+            launch_rows<K, LTR, TM_ROWS>(src, dst, n, p.hi, p.R, p.flip, s);
+        } else if (p.kind == KIND_SPAN) {
+            launch_rows<K, LTR, TM_SPAN>(src, dst, n, p.hi, p.R, true, s);
         } else {
             launch_stream<K, LT, TM_MERGE, 0, false, false>(src, dst, n, tm, s);
         }

@@ -13,7 +13,8 @@ enum Kind : int {
     KIND_TILE_MERGE = 2,  // strides < tile of one level, LDS tile
     KIND_MERGE_SPLIT = 3, // compare-split merge (keep lowest/highest n)
     KIND_OTHER = 4,       // f64 transform, fills, checks
-    KIND_COUNT = 5
+    KIND_SPAN = 5,        // tail of one level + head of the next, row tile
+    KIND_COUNT = 6
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with
@@ -79,5 +80,9 @@ hipError_t fill_splitmix_u64(uint64_t* out, int64_t n, uint64_t seed, int64_t g0
 
 // Tile geometry per key type (exported for documentation/tests).
 int tile_log2(int key_bytes);
+
+// The HBM pass plan local_sort runs for n keys of key_bytes (4 or 8): writes
+// up to max passes as 4 ints each (kind, hi, R, flip) and returns the count.
+int plan_passes(int64_t n, int key_bytes, int* out, int max);
 
 }  // namespace misort

@@ -18,6 +18,8 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_PERSIST", persist);
     env("MISORT_GRID_MULT", grid_mult);
     env("MISORT_PINGPONG", pingpong);
+    env("MISORT_SPAN", span);
+    env("MISORT_ROW_BYTES_LOG2", row_bytes_log2);
     if (tile_u32 != 14) tile_u32 = 15;
     if (rows_tile_u32 != 14 && tile_u32 == 15) rows_tile_u32 = 15;
     if (tile_u32 != 15) rows_tile_u32 = 14;
@@ -34,6 +36,31 @@ const PlanKnobs& plan_knobs() {
 int tile_log2(int key_bytes) {
     const int u32 = plan_knobs().tile_u32;
     return key_bytes == 4 ? u32 : u32 - 1;
+}
+
+int plan_passes(int64_t n, int key_bytes, int* out, int max) {
+    if (n <= 0) return 0;
+    constexpr int S = KT<uint32_t>::LT_SMALL;
+    const PlanKnobs& kn = plan_knobs();
+    const bool big = kn.tile_u32 == 15, rbig = kn.rows_tile_u32 == 15;
+    std::vector<Pass> ps;
+    if (key_bytes == 4) {
+        ps = big && rbig ? plan_for<uint32_t, S + 1, S + 1>(n)
+             : big       ? plan_for<uint32_t, S + 1, S>(n)
+                         : plan_for<uint32_t, S, S>(n);
+    } else {
+        ps = big && rbig ? plan_for<uint64_t, S, S>(n)
+             : big       ? plan_for<uint64_t, S, S - 1>(n)
+                         : plan_for<uint64_t, S - 1, S - 1>(n);
+    }
+    const int np = (int)ps.size();
+    for (int i = 0; i < np && i < max; ++i) {
+        out[4 * i + 0] = ps[i].kind;
+        out[4 * i + 1] = ps[i].hi;
+        out[4 * i + 2] = ps[i].R;
+        out[4 * i + 3] = ps[i].flip;
+    }
+    return np;
 }
 
 namespace {

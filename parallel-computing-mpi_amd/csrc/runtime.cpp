@@ -1254,4 +1254,10 @@ int misort_profile_read(misort_ctx* c, int kind, int64_t* launches, double* tota
 
 int misort_tile_log2(int key_bytes_) { return misort::tile_log2(key_bytes_); }
 
+int misort_plan(int64_t n, int key_bytes, int* passes, int max_passes) {
+    if (key_bytes != 4 && key_bytes != 8) return fail(MISORT_E_INVALID, "key_bytes must be 4 or 8");
+    if (max_passes > 0 && !passes) return fail(MISORT_E_INVALID, "null passes");
+    return misort::plan_passes(n, key_bytes, passes, max_passes < 0 ? 0 : max_passes);
+}
+
 }  // extern "C"

@@ -18,12 +18,12 @@ import os
 
 __all__ = [
     "U32", "U64", "F64", "MisortError", "NotPowerOfTwo", "NativeLibraryMissing",
-    "library_path", "lib", "Context", "Group", "block_sizes", "schedule", "tile_log2",
+    "library_path", "lib", "Context", "Group", "block_sizes", "schedule", "tile_log2", "plan",
     "sample_indices", "exchange_count",
 ]
 
 U32, U64, F64 = 0, 1, 2
-KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other"]
+KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other", "span_pass"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
@@ -86,6 +86,7 @@ def lib():
         "misort_profile_read": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_tile_log2": ([i32], i32),
+        "misort_plan": ([ctypes.c_int64, i32, ctypes.POINTER(i32), i32], i32),
         "misort_group_create": ([i32, ctypes.POINTER(vp)], i32),
         "misort_group_destroy": ([vp], i32),
         "misort_comm_init_group": ([vp, vp, i32], i32),
@@ -147,6 +148,16 @@ def exchange_count(samples_min, n_min, samples_max, n_max):
 
 def tile_log2(key_bytes):
     return int(lib().misort_tile_log2(key_bytes))
+
+
+def plan(n, key_bytes=4):
+    """The HBM pass plan of a local sort of n keys: [(kind_name, hi, R, flip)]."""
+    np_ = lib().misort_plan(n, key_bytes, None, 0)
+    _check(np_ if np_ < 0 else 0)
+    buf = (ctypes.c_int32 * (4 * max(np_, 1)))()
+    lib().misort_plan(n, key_bytes, buf, np_)
+    return [(KIND_NAMES[buf[4 * i]], buf[4 * i + 1], buf[4 * i + 2], bool(buf[4 * i + 3]))
+            for i in range(np_)]
 
 
 class Group:

@@ -1,0 +1,107 @@
+"""The HBM pass planner (bitonic.h plan_span / plan_levels) on the CPU.
+
+Every plan misort_plan() returns is replayed stage by stage on a numpy model of
+the flip-formulation bitonic network (the network local_sort runs in place of
+the reference's std::sort, psort.cc:175).  A plan is right when
+  * its stages, concatenated, are exactly the network's stage sequence, and
+  * replaying them (with the virtual all-ones padding for non-power-of-two n)
+    sorts random keys like np.sort.
+No device is touched: misort_plan is host-only."""
+import numpy as np
+import pytest
+
+import misort
+
+KIND_SORT, KIND_ROWS, KIND_MERGE, KIND_SPAN = "tile_sort", "global_pass", "tile_merge", "span_pass"
+
+
+def ceil_log2(n):
+    return max(0, int(n - 1).bit_length())
+
+
+def network(k, lt):
+    """The stage sequence after the SORT pass: (level m, bit b), flip when b = m-1."""
+    return [(m, b) for m in range(lt + 1, k + 1) for b in range(m - 1, -1, -1)]
+
+
+def plan_stages(plan, lt):
+    """Stages the plan's passes run after the SORT pass, as (level, bit)."""
+    out = []
+    for kind, hi, r, flip in plan[1:]:
+        if kind == KIND_ROWS:
+            # a ROWS pass runs bits hi..hi-R+1 of the level whose stages they are;
+            # the level is known from the flip (hi = m-1) or from the sequence so far
+            m = hi + 1 if flip else out[-1][0]
+            out += [(m, b) for b in range(hi, hi - r, -1)]
+        elif kind == KIND_MERGE:
+            m = out[-1][0] if out else lt + 1
+            out += [(m, b) for b in range(lt - 1, -1, -1)]
+        elif kind == KIND_SPAN:
+            m = hi  # tail of level hi, then the head of level hi + 1
+            out += [(m, b) for b in range(lt - r - 1, -1, -1)]
+            out += [(m + 1, b) for b in range(m, m - r, -1)]
+        else:
+            raise AssertionError(kind)
+    return out
+
+
+def stage(x, m, b):
+    """One network stage on the padded array x (length 2^k): flip (b = m-1) pairs i
+    with i ^ (2^m - 1), a half-cleaner pairs i with i ^ 2^b; min to the lower index."""
+    n = x.size
+    i = np.arange(n)
+    j = i ^ ((1 << m) - 1) if b == m - 1 else i ^ (1 << b)
+    lo = i < j
+    a, c = x[i[lo]], x[j[lo]]
+    x[i[lo]] = np.minimum(a, c)
+    x[j[lo]] = np.maximum(a, c)
+
+
+def replay(keys, plan, lt):
+    k = ceil_log2(keys.size)
+    x = np.full(1 << k, np.iinfo(keys.dtype).max, dtype=keys.dtype)
+    x[: keys.size] = keys
+    # SORT pass: levels 1..min(lt, k) inside each 2^lt tile
+    for m in range(1, min(lt, k) + 1):
+        for b in range(m - 1, -1, -1):
+            stage(x, m, b)
+    for m, b in plan_stages(plan, lt):
+        stage(x, m, b)
+    return x[: keys.size]
+
+
+SIZES = [1, 2, 31, 1000, (1 << 15) - 3, 1 << 15, (1 << 15) + 1, 1 << 16, 100003, 1 << 18,
+         (1 << 20) - 7, 1 << 24, 1 << 28, (1 << 29) - 3, 1 << 30, 1 << 31]
+
+
+@pytest.mark.parametrize("key_bytes", [4, 8])
+@pytest.mark.parametrize("n", SIZES)
+def test_plan_covers_network(n, key_bytes):
+    lt = misort.tile_log2(key_bytes)
+    p = misort.plan(n, key_bytes)
+    assert p[0][0] == KIND_SORT
+    k = ceil_log2(n)
+    assert plan_stages(p, lt) == network(k, lt)
+    for kind, hi, r, flip in p[1:]:
+        if kind in (KIND_ROWS, KIND_SPAN):
+            assert 1 <= r <= lt - 5  # rows keep >= 32 consecutive keys (128 B for u32)
+
+
+def test_plan_pass_counts():
+    # 2^30 u32: 1 SORT + 29 passes (the level-by-level plan needs 1 + 35)
+    assert len(misort.plan(1 << 30, 4)) == 30
+    assert len(misort.plan(1 << 28, 4)) == 25
+    assert len(misort.plan(1 << 24, 4)) == 15
+    assert any(k == KIND_SPAN for k, *_ in misort.plan(1 << 30, 4))
+
+
+@pytest.mark.parametrize("key_bytes", [4, 8])
+@pytest.mark.parametrize("n", [(1 << 15) + 1, 1 << 16, 100003, (1 << 18) - 5, 1 << 19])
+def test_plan_replay_sorts(n, key_bytes):
+    lt = misort.tile_log2(key_bytes)
+    dt = np.uint32 if key_bytes == 4 else np.uint64
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, np.iinfo(dt).max, size=n, dtype=dt, endpoint=True)
+    keys[::7] = keys[3]  # duplicates
+    got = replay(keys, misort.plan(n, key_bytes), lt)
+    np.testing.assert_array_equal(got, np.sort(keys))
