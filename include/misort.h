@@ -213,6 +213,14 @@ int misort_tile_log2(int key_bytes);
  * negative status).  Host-only; no device is touched. */
 int misort_plan(int64_t n, int key_bytes, int* passes, int max_passes);
 
+/* Tooling: average device time (ms, HIP events on the context stream) of ONE
+ * HBM pass of the given shape (kind/hi/R/flip as misort_plan reports them)
+ * over n keys, alternating in -> out and out -> in for `reps` launches.  The
+ * keys are scrambled by it (a single pass is not a sort).  Feeds the
+ * planner's measured cost table (tools/pass_costs.py). */
+int misort_pass_probe(misort_ctx* ctx, int dtype, const void* in, void* out, int64_t n, int kind,
+                      int hi, int r, int flip, int reps, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

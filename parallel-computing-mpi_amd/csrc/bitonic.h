@@ -30,9 +30,11 @@
 #pragma once
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "kernels.h"
+#include "pass_costs.h"
 
 namespace misort {
 
@@ -52,10 +54,12 @@ namespace misort {
 //   MISORT_SPAN            1 (default): plan passes across level boundaries with
 //                          SPAN passes (fewest passes); 0: one MERGE per level;
 //   MISORT_ROW_BYTES_LOG2  shortest row run a ROWS/SPAN tile may use (default 8:
-//                          256 B; 7 allows 128-B rows).
+//                          256 B; 7 allows 128-B rows);
+//   MISORT_COST_TABLE      1 (default): the planner prices passes from the
+//                          measured table (pass_costs.h); 0: from the model.
 struct PlanKnobs {
     int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
-    int span = 1, row_bytes_log2 = 8;
+    int span = 1, row_bytes_log2 = 8, cost_table = 1;
     PlanKnobs();
 };
 const PlanKnobs& plan_knobs();
@@ -208,21 +212,34 @@ __device__ __forceinline__ bool tile_full(const TileMap& m, int64_t tile, int64_
     }
 }
 
-// Slot k of lane t: virtual vector start, and whether it is held mirrored.
+// Slot k of lane t: the lane whose vector it holds (mirrored slots: the
+// mirror lane, components reversed).
 template <typename K, int LT, bool MIRROR>
 __device__ __forceinline__ int slot_lane(int k, int t) {
     typedef TileGeo<K, LT> G;
     return (MIRROR && k >= G::LOADS / 2) ? (G::NT - 1 - t) : t;
 }
 
-template <typename K, int LT, int MODE, bool MIRROR, bool ORD>
+// Virtual start of the vector of slot k, lane t, when the KB slot bits sit at
+// virtual bits [SL, SL+KB): components are bits [0, VB), the lane fills the
+// bits below and above the slot window.  SL = LT-KB is the plain layout
+// (k*NT + t)*V.  Any SL >= VB+5 keeps 32 consecutive lanes on consecutive
+// vectors (coalesced HBM access, conflict-free LDS access under pad()).
+template <typename K, int LT, int SL>
+__device__ __forceinline__ int place(int k, int t) {
+    typedef TileGeo<K, LT> G;
+    constexpr int LB = SL - G::VB;  // lane bits below the slot window
+    return ((t & ((1 << LB) - 1)) << G::VB) | (k << SL) | ((t >> LB) << (SL + G::KB));
+}
+
+template <typename K, int LT, int MODE, int SL, bool MIRROR, bool ORD>
 __device__ __forceinline__ void tile_fetch(K (*pre)[KT<K>::V], const K* src, const TileMap& m,
                                            int64_t tile, int64_t n, int t) {
     typedef TileGeo<K, LT> G;
     const bool full = tile_full<LT, MODE>(m, tile, n);
 #pragma unroll
     for (int k = 0; k < G::LOADS; ++k) {
-        const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+        const int e = place<K, LT, SL>(k, slot_lane<K, LT, MIRROR>(k, t));
         const int64_t gi = tile_index<LT, MODE>(m, tile, e);
         typename KT<K>::vec x;
         if (full) {
@@ -308,6 +325,201 @@ __device__ __forceinline__ void sort_levels(K* s, int t) {
     }
 }
 
+// Stages on the slot bits of register-held vectors: relative slot bits
+// TOP..TOP-CNT+1, the first one a flip if FLIP (the flip complements every
+// slot bit; mirrored upper slots complete it to the tile's own v <-> ~v).
+template <typename K, int LOADS, int TOP, int CNT, bool FLIP>
+__device__ __forceinline__ void slot_stages(K (*w)[KT<K>::V]) {
+#pragma unroll
+    for (int i = 0; i < CNT; ++i) {
+        const int r = TOP - i;
+        const bool fl = FLIP && i == 0;
+#pragma unroll
+        for (int k = 0; k < LOADS; ++k) {
+            if (k & (1 << r)) continue;
+            const int p = fl ? (k ^ ((2 << r) - 1)) : (k | (1 << r));
+#pragma unroll
+            for (int j = 0; j < KT<K>::V; ++j) cx(w[k][j], w[p][j]);
+        }
+    }
+}
+
+// Compile-time schedule of one non-SORT pass (host and device).  A pass runs a
+// stage sequence on virtual bits; stages on slot bits run in registers, the
+// rest in 5-bit LDS phases.  Two free choices cut LDS phases:
+//   * the load slot window SL: a SPAN pass puts it on the top KB bits of its
+//     tail, so those stages run before the LDS write;
+//   * the final-read slot window SF: the LAST stages of the pass (the low head
+//     bits of a SPAN or ROWS pass) run in registers after the LDS read; a
+//     head of <= KB stages runs there entirely, its flip through mirrored
+//     upper slots.
+// Sequences: ROWS  LT-1 .. LT-R (flip first if FLIP);
+//            MERGE LT-1 .. 0;
+//            SPAN  LT-R-1 .. 0, then flip(LT-1), LT-2 .. LT-R.
+struct ProgGeo {
+    int LT, KB, VB, MODE, R;
+    bool FLIP;
+    int POSTCAP;  // most final-read register stages (register budget: 2 when a
+                  // persistent grid keeps the next tile's 32 keys in flight)
+};
+struct ProgPlan {
+    int SL;            // load slot window
+    bool MLOAD;        // mirrored upper slots at load (flip on slot bits)
+    int PRE, PRE_TOP;  // register stages after the load (relative top, count)
+    bool PRE_FLIP;
+    bool DIRECT;       // every stage in registers: no LDS at all
+    int T_HI, T_LO;    // first LDS range (no flip); empty when T_HI < T_LO
+    int H_HI, H_LO;    // second LDS range, flip first (SPAN head); empty when H_HI < H_LO
+    int SF;            // final-read slot window
+    bool MFIN;         // mirrored upper slots at the final read
+    int POST, POST_TOP;
+    bool POST_FLIP;
+    bool COMP;         // component-bit stages after the final read (MERGE)
+    int phases;        // LDS phases (5-bit windows)
+};
+__host__ __device__ constexpr int windows(int hi, int lo) { return hi < lo ? 0 : (hi - lo + 5) / 5; }
+// Build-time switches of the schedule choices (A/B probes: tools/build_variant.sh).
+// Measured (profiles/r01/ab/prog_variants.txt): the register tail/head tricks
+// make SPAN passes slower (shorter load runs; spills beside the persistent
+// prefetch), the final-read window makes ROWS R=4..8 passes faster (R=6: no
+// LDS phase at all) -- so SPAN keeps its LDS-only schedule by default.
+#ifndef MISORT_SPAN_PRE
+#define MISORT_SPAN_PRE 0
+#endif
+#ifndef MISORT_SPAN_POST
+#define MISORT_SPAN_POST 0
+#endif
+#ifndef MISORT_ROWS_POST
+#define MISORT_ROWS_POST 1
+#endif
+__host__ __device__ constexpr ProgPlan prog_plan(ProgGeo g) {
+    ProgPlan p{};
+    const int TOPS = g.LT - g.KB, MINW = g.VB + 5;
+    const int cap = g.POSTCAP < g.KB ? g.POSTCAP : g.KB;
+    p.SL = TOPS;
+    p.SF = TOPS;
+    p.T_HI = -1; p.T_LO = 0; p.H_HI = -1; p.H_LO = 0;
+    if (g.MODE == TM_MERGE) {
+        p.PRE = g.KB; p.PRE_TOP = g.KB - 1;
+        p.T_HI = TOPS - 1; p.T_LO = g.VB;
+        p.COMP = true;
+    } else if (g.MODE == TM_ROWS) {
+        p.MLOAD = g.FLIP;
+        p.PRE = g.R < g.KB ? g.R : g.KB; p.PRE_TOP = g.KB - 1; p.PRE_FLIP = g.FLIP;
+        if (g.R <= g.KB) {
+            p.DIRECT = true;
+        } else {
+            // stages after the load: TOPS-1 .. last; the final window starts at last
+            const int last = g.LT - g.R;
+            const int rest = TOPS - last;
+            const int q = rest < cap ? rest : cap;
+            if (MISORT_ROWS_POST && last >= MINW && q > 0) {
+                p.SF = last;
+                p.POST = q; p.POST_TOP = q - 1;
+                p.T_HI = TOPS - 1; p.T_LO = last + q;
+            } else {
+                p.T_HI = TOPS - 1; p.T_LO = last;
+            }
+        }
+    } else if (g.MODE == TM_SPAN) {
+        const int TA = g.LT - g.R;
+        if (MISORT_SPAN_PRE && TA - g.KB >= MINW) {
+            p.SL = TA - g.KB;
+            p.PRE = g.KB; p.PRE_TOP = g.KB - 1;
+            p.T_HI = TA - g.KB - 1;
+        } else {
+            p.T_HI = TA - 1;
+        }
+        p.T_LO = 0;
+        if (!MISORT_SPAN_POST) {
+            p.H_HI = g.LT - 1; p.H_LO = TA;
+        } else if (g.R <= cap) {
+            // the whole head (flip first) on the top slot bits, mirrored read
+            p.MFIN = true;
+            p.POST = g.R; p.POST_TOP = g.KB - 1; p.POST_FLIP = true;
+        } else if (TA >= MINW && cap > 0) {
+            // the head's last `cap` stages in registers, the rest in LDS
+            p.SF = TA;
+            p.POST = cap; p.POST_TOP = cap - 1;
+            p.H_HI = g.LT - 1; p.H_LO = TA + cap;
+        } else {
+            p.H_HI = g.LT - 1; p.H_LO = TA;
+        }
+    }
+    p.phases = windows(p.T_HI, p.T_LO) + windows(p.H_HI, p.H_LO);
+    return p;
+}
+
+// Slot-pairing masks of a register stage list: stage i of TOP..TOP-CNT+1 pairs
+// slot k with k ^ pmask(i) (a flip complements every slot bit up to TOP).
+__host__ __device__ constexpr int pmask(int i, int top, bool flip) {
+    return (flip && i == 0) ? ((2 << top) - 1) : (1 << (top - i));
+}
+__host__ __device__ constexpr int psub(int S, int cnt, int top, bool flip) {
+    int x = 0;
+    for (int i = 0; i < cnt; ++i)
+        if ((S >> i) & 1) x ^= pmask(i, top, flip);
+    return x;
+}
+// k is the smallest slot of its group (the slots the stage list connects).
+__host__ __device__ constexpr bool pgroup_rep(int k, int cnt, int top, bool flip) {
+    for (int S = 1; S < (1 << cnt); ++S)
+        if ((k ^ psub(S, cnt, top, flip)) < k) return false;
+    return true;
+}
+
+// LDS -> registers (final slot window SF, mirrored upper slots if MF) -> the
+// pass's last register stages -> HBM.  Slots are handled one stage-connected
+// group at a time, so only 2^CNT vectors are live.
+template <typename K, int LT, int MODE, int SF, bool MF, int TOP, int CNT, bool FLIP, bool COMP>
+__device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m, int64_t tile, int64_t n,
+                                            bool full, int t) {
+    typedef TileGeo<K, LT> G;
+    constexpr int NG = 1 << CNT;
+#pragma unroll
+    for (int k0 = 0; k0 < G::LOADS; ++k0) {
+        if (!pgroup_rep(k0, CNT, TOP, FLIP)) continue;
+        K w[NG][G::V];
+#pragma unroll
+        for (int S = 0; S < NG; ++S) {
+            const int k = k0 ^ psub(S, CNT, TOP, FLIP);
+            const bool mk = MF && k >= G::LOADS / 2;
+            const int e = place<K, LT, SF>(k, slot_lane<K, LT, MF>(k, t));
+#pragma unroll
+            for (int j = 0; j < G::V; ++j) w[S][j] = s[pad(e + (mk ? G::V - 1 - j : j))];
+        }
+#pragma unroll
+        for (int i = 0; i < CNT; ++i) {
+            const int r = TOP - i;
+#pragma unroll
+            for (int S = 0; S < NG; ++S) {
+                if ((S >> i) & 1) continue;
+                const int kA = k0 ^ psub(S, CNT, TOP, FLIP);
+                const bool a_low = !((kA >> r) & 1);  // the lower virtual index takes the minimum
+                const int lo = a_low ? S : (S | (1 << i)), hi = a_low ? (S | (1 << i)) : S;
+#pragma unroll
+                for (int j = 0; j < G::V; ++j) cx(w[lo][j], w[hi][j]);
+            }
+        }
+#pragma unroll
+        for (int S = 0; S < NG; ++S) {
+            if constexpr (COMP) {
+#pragma unroll
+                for (int r = G::VB - 1; r >= 0; --r)
+#pragma unroll
+                    for (int j = 0; j < G::V; ++j)
+                        if (!(j & (1 << r))) cx(w[S][j], w[S][j | (1 << r)]);
+            }
+            const int k = k0 ^ psub(S, CNT, TOP, FLIP);
+            const bool mk = MF && k >= G::LOADS / 2;
+            K x[G::V];
+#pragma unroll
+            for (int j = 0; j < G::V; ++j) x[j] = mk ? w[S][G::V - 1 - j] : w[S][j];
+            store_slot<K, LT, MODE>(out, m, tile, n, full, place<K, LT, SF>(k, slot_lane<K, LT, MF>(k, t)), x);
+        }
+    }
+}
+
 // PERSIST: the grid is smaller than the tile list and every workgroup walks
 // tiles with the next tile's loads in flight; otherwise one tile per workgroup
 // (no prefetch registers live across the LDS phases).
@@ -315,54 +527,41 @@ template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD, bool PERSIST
 __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_stream(
     const K* in, K* out, int64_t n, TileMap m) {
     typedef TileGeo<K, LT> G;
-    constexpr bool MIRROR = MODE == TM_ROWS && FLIP;
-    // slot-bit strides done in registers before the LDS write
-    constexpr int PRE = MODE == TM_MERGE ? G::KB : MODE == TM_ROWS ? (R < G::KB ? R : G::KB) : 0;
+    constexpr ProgPlan P = prog_plan(ProgGeo{LT, G::KB, G::VB, MODE, R, FLIP, PERSIST ? 2 : G::KB});
+    constexpr int SL = MODE == TM_SORT ? LT - G::KB : P.SL;
     __shared__ K s[pad(G::T)];
     const int t = threadIdx.x;
     K pre[G::LOADS][G::V];
     int64_t tile = blockIdx.x;
     if (tile >= m.ntiles) return;
-    tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, tile, n, t);
+    tile_fetch<K, LT, MODE, SL, P.MLOAD, ORD>(pre, in, m, tile, n, t);
     for (; tile < m.ntiles; tile += gridDim.x) {
-#pragma unroll
-        for (int i = 0; i < PRE; ++i) {
-            const int r = G::KB - 1 - i;
-            const bool fl = MIRROR && i == 0;
-#pragma unroll
-            for (int k = 0; k < G::LOADS; ++k) {
-                if (k & (1 << r)) continue;
-                const int p = fl ? (k ^ (G::LOADS - 1)) : (k | (1 << r));
-#pragma unroll
-                for (int j = 0; j < G::V; ++j) cx(pre[k][j], pre[p][j]);
-            }
-        }
+        slot_stages<K, G::LOADS, P.PRE_TOP, P.PRE, P.PRE_FLIP>(pre);
         const bool full = tile_full<LT, MODE>(m, tile, n);
-        if constexpr (MODE == TM_ROWS && R <= G::KB) {
+        if constexpr (P.DIRECT) {
             // every stride of this pass was a slot bit: store straight from registers
 #pragma unroll
             for (int k = 0; k < G::LOADS; ++k) {
                 K w[G::V];
-                const bool mk = MIRROR && k >= G::LOADS / 2;
+                const bool mk = P.MLOAD && k >= G::LOADS / 2;
 #pragma unroll
                 for (int j = 0; j < G::V; ++j) w[j] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
-                store_slot<K, LT, MODE>(out, m, tile, n, full,
-                                        (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V, w);
+                store_slot<K, LT, MODE>(out, m, tile, n, full, place<K, LT, SL>(k, slot_lane<K, LT, P.MLOAD>(k, t)), w);
             }
             const int64_t nxt = tile + gridDim.x;
-            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, SL, P.MLOAD, ORD>(pre, in, m, nxt, n, t);
         } else {
             // registers -> LDS (mirrored slots to their own virtual position)
 #pragma unroll
             for (int k = 0; k < G::LOADS; ++k) {
-                const bool mk = MIRROR && k >= G::LOADS / 2;
-                const int e = (k * G::NT + slot_lane<K, LT, MIRROR>(k, t)) * G::V;
+                const bool mk = P.MLOAD && k >= G::LOADS / 2;
+                const int e = place<K, LT, SL>(k, slot_lane<K, LT, P.MLOAD>(k, t));
 #pragma unroll
                 for (int j = 0; j < G::V; ++j) s[pad(e + j)] = mk ? pre[k][G::V - 1 - j] : pre[k][j];
             }
             __syncthreads();
             const int64_t nxt = tile + gridDim.x;
-            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, MIRROR, ORD>(pre, in, m, nxt, n, t);
+            if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, SL, P.MLOAD, ORD>(pre, in, m, nxt, n, t);
             if constexpr (MODE == TM_SORT) {
                 {   // levels 1..5: window [0,5), 32 consecutive keys per lane
                     K v[32];
@@ -379,33 +578,14 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
                 }
                 __syncthreads();
                 sort_levels<K, 6, LT>(s, t);
-            } else if constexpr (MODE == TM_MERGE) {
-                lds_range<K, LT - G::KB - 1, G::VB, false>(s, t);
-            } else if constexpr (MODE == TM_SPAN) {
-                // tail of level m on the row-run bits, then level m+1's flip
-                // (v <-> ~v: the tile's mirrored rows make it the global
-                // mirror) and its half-cleaners on the row bits
-                lds_range<K, LT - R - 1, 0, false>(s, t);
-                lds_range<K, LT - 1, LT - R, true>(s, t);
             } else {
-                lds_range<K, LT - G::KB - 1, LT - R, false>(s, t);
+                lds_range<K, P.T_HI, P.T_LO, false>(s, t);
+                lds_range<K, P.H_HI, P.H_LO, true>(s, t);
             }
-            // LDS -> registers -> HBM; in a merge the vector-component strides run here
-#pragma unroll
-            for (int k = 0; k < G::LOADS; ++k) {
-                const int e = (k * G::NT + t) * G::V;
-                K w[G::V];
-#pragma unroll
-                for (int j = 0; j < G::V; ++j) w[j] = s[pad(e + j)];
-                if constexpr (MODE == TM_MERGE) {
-#pragma unroll
-                    for (int r = G::VB - 1; r >= 0; --r)
-#pragma unroll
-                        for (int j = 0; j < G::V; ++j)
-                            if (!(j & (1 << r))) cx(w[j], w[j | (1 << r)]);
-                }
-                store_slot<K, LT, MODE>(out, m, tile, n, full, e, w);
-            }
+            // LDS -> registers (final slot window) -> last stages -> HBM
+            constexpr int SF = MODE == TM_SORT ? LT - G::KB : P.SF;
+            final_store<K, LT, MODE, SF, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n,
+                                                                                        full, t);
             __syncthreads();
         }
         if constexpr (!PERSIST) break;
@@ -528,11 +708,47 @@ inline std::vector<Pass> plan_levels(int k, int LT, int rmax) {
 //   SPAN  bits LT-R-1..0 of level m, then bits m..m-R+1 of level m+1 (the
 //         flip first): a ROWS tile of R row bits whose 2^(LT-R)-key rows hold
 //         the tail's bits.
-// Dynamic programming over the sequence minimises the modelled time: every
-// pass costs one HBM sweep, ROWS tiles with the shortest (2^cmin-key) rows and
-// SPAN passes (more LDS phases) a little more.  For 2^30 u32 keys this is
-// 1 + 29 passes instead of the level-by-level plan's 1 + 35.
-inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin) {
+// Dynamic programming over the sequence minimises the modelled time: one HBM
+// sweep per pass, plus a little per LDS phase of the pass's schedule
+// (prog_plan) and for the shortest (2^cmin-key) rows.  For 2^30 u32 keys this
+// is 1 + 29 passes instead of the level-by-level plan's 1 + 35.
+inline double model_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin) {
+    const bool persist = (plan_knobs().persist >> mode) & 1;
+    const ProgPlan pp = prog_plan(ProgGeo{LT, KB, VB, mode, R, flip, persist ? 2 : KB});
+    const bool short_rows = (mode == TM_ROWS || mode == TM_SPAN) && LT - R <= cmin;
+    return 1.0 + 0.035 * pp.phases + (short_rows ? 0.03 : 0.0);
+}
+
+// Cost of one pass in "median pass" units: the measured table (pass_costs.h,
+// tools/pass_costs.py: every shape timed alone on an MI355X at 2^logn keys;
+// the closest logn to this sort's 2^k is used) where it has the shape, else
+// the model above.  The table captures what the model cannot: rows at some
+// power-of-two strides run up to 40 % slower than at others (HBM channel
+// aliasing), so the planner steers around them.
+inline double pass_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin, int kb, int hi, int k) {
+    const int kind = mode == TM_ROWS ? KIND_GLOBAL : mode == TM_SPAN ? KIND_SPAN : KIND_TILE_MERGE;
+    if (plan_knobs().cost_table) {
+        int best = -1, bd = 1 << 30;
+        for (int i = 0; i < kNumPassCosts; ++i) {
+            const PassCost& e = kPassCosts[i];
+            if (e.key_bytes != kb || e.kind != kind || e.R != R || (e.flip != 0) != flip || e.hi != hi) continue;
+            const int d = e.logn > k ? e.logn - k : k - e.logn;
+            if (d < bd) { bd = d; best = i; }
+        }
+        if (best >= 0) {
+            // unit: the median of the table's passes at that size
+            const int ln = kPassCosts[best].logn;
+            std::vector<float> v;
+            for (int i = 0; i < kNumPassCosts; ++i)
+                if (kPassCosts[i].key_bytes == kb && kPassCosts[i].logn == ln) v.push_back(kPassCosts[i].us);
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            return kPassCosts[best].us / v[v.size() / 2];
+        }
+    }
+    return model_cost(LT, KB, VB, mode, R, flip, cmin);
+}
+
+inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin, int KB, int VB, int kb) {
     struct St { int m, b; };
     std::vector<St> seq;
     for (int m = LT + 1; m <= k; ++m)
@@ -556,15 +772,18 @@ inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin) {
             for (int R = 1; R <= rmax && LT - R >= cmin; ++R) {
                 const int lo = b - R + 1;
                 if (lo < LT - R) break;
-                take(p + R, 1.0 + (LT - R == cmin ? 0.05 : 0.0), Pass{KIND_GLOBAL, b, R, b == m - 1});
+                take(p + R, pass_cost(LT, KB, VB, TM_ROWS, R, b == m - 1, cmin, kb, b, k),
+                     Pass{KIND_GLOBAL, b, R, b == m - 1});
             }
         } else if (b == LT - 1) {
-            take(p + LT, 0.97, Pass{KIND_TILE_MERGE, LT - 1, 0, false});
+            take(p + LT, pass_cost(LT, KB, VB, TM_MERGE, 0, false, cmin, kb, LT - 1, k),
+                 Pass{KIND_TILE_MERGE, LT - 1, 0, false});
         }
         if (b < LT && m < k) {
             const int R = LT - (b + 1);
             if (R >= 1 && R <= rmax && LT - R >= cmin)
-                take(p + (b + 1) + R, 1.02, Pass{KIND_SPAN, m, R, true});
+                take(p + (b + 1) + R, pass_cost(LT, KB, VB, TM_SPAN, R, true, cmin, kb, m, k),
+                     Pass{KIND_SPAN, m, R, true});
         }
     }
     std::vector<Pass> ps;
@@ -574,8 +793,8 @@ inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin) {
     return ps;
 }
 
-inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span) {
-    return span ? plan_span(k, LT, rmax, cmin) : plan_levels(k, LT, rmax);
+inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span, int KB, int VB, int kb) {
+    return span ? plan_span(k, LT, rmax, cmin, KB, VB, kb) : plan_levels(k, LT, rmax);
 }
 
 // The plan local_sort_lt runs for n keys (shared with plan_passes()).
@@ -585,7 +804,29 @@ std::vector<Pass> plan_for(int64_t n) {
     const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
     int cmin = kn.row_bytes_log2 - (sizeof(K) == 4 ? 2 : 3);
     if (cmin < 5) cmin = 5;
-    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR);
+    typedef TileGeo<K, LT> G;
+    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K));
+}
+
+// One pass of a plan over n keys, src -> dst.
+template <typename K, int LT, int LTR>
+void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hipStream_t s) {
+    TileMap tm{};
+    tm.ntiles = (n + (1 << LT) - 1) >> LT;
+    if (p.kind == KIND_TILE_SORT) {
+        if constexpr (sizeof(K) == 8) {
+            if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
+            else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+        } else {
+            launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+        }
+    } else if (p.kind == KIND_GLOBAL) {
+        launch_rows<K, LTR, TM_ROWS>(src, dst, n, p.hi, p.R, p.flip, s);
+    } else if (p.kind == KIND_SPAN) {
+        launch_rows<K, LTR, TM_SPAN>(src, dst, n, p.hi, p.R, true, s);
+    } else {
+        launch_stream<K, LT, TM_MERGE, 0, false, false>(src, dst, n, tm, s);
+    }
 }
 
 // LT: SORT/MERGE tile; LTR: ROWS tile.
@@ -597,28 +838,13 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
     const int np = (int)ps.size();
     const bool pp = kn.pingpong && scratch != nullptr && scratch != out && scratch != in;
     const double bytes = 2.0 * (double)n * sizeof(K);
-    TileMap tm{};
-    tm.ntiles = (n + (1 << LT) - 1) >> LT;
     const K* src = in;
     for (int i = 0; i < np; ++i) {
         // ping-pong: pass i writes `out` iff an even number of passes follow it
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
-        if (p.kind == KIND_TILE_SORT) {
-            if constexpr (sizeof(K) == 8) {
-                if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
-                else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
-            } else {
-                launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
-            }
-        } else if (p.kind == KIND_GLOBAL) {
-            launch_rows<K, LTR, TM_ROWS>(src, dst, n, p.hi, p.R, p.flip, s);
-        } else if (p.kind == KIND_SPAN) {
-            launch_rows<K, LTR, TM_SPAN>(src, dst, n, p.hi, p.R, true, s);
-        } else {
-            launch_stream<K, LT, TM_MERGE, 0, false, false>(src, dst, n, tm, s);
-        }
+        launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s);
         src = dst;
     }
     return hipGetLastError();
@@ -638,6 +864,22 @@ hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, h
     if (big && rbig) return local_sort_lt<K, S + 1, S + 1>(in, out, n, ord_in, scratch, s, hook);
     if (big) return local_sort_lt<K, S + 1, S>(in, out, n, ord_in, scratch, s, hook);
     return local_sort_lt<K, S, S>(in, out, n, ord_in, scratch, s, hook);
+}
+
+// One pass of any shape (pass-cost probes, tools/pass_costs.py).
+template <typename K>
+hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int flip, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    constexpr int S = KT<K>::LT_SMALL;
+    const PlanKnobs& kn = plan_knobs();
+    const Pass p{(Kind)kind, hi, R, flip != 0};
+    if (kind == KIND_GLOBAL || kind == KIND_SPAN) {
+        if (R < 1 || R > S + 1 - 5 || hi - R + 1 < S + 1 - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
+            return hipErrorInvalidValue;
+    }
+    if (kn.tile_u32 == 15 && kn.rows_tile_u32 == 15) launch_pass<K, S + 1, S + 1>(in, out, n, p, false, s);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 }  // namespace misort

@@ -36,6 +36,12 @@ template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                       LaunchHook* hook);
 
+// One HBM pass of the given shape (kind KIND_TILE_SORT / KIND_GLOBAL /
+// KIND_SPAN / KIND_TILE_MERGE, hi, R, flip as in the plan) over n keys: the
+// pass-cost probe behind the planner's cost table.
+template <typename K>
+hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int flip, hipStream_t s);
+
 // Compare-split merge (device half of psort.cc:116-164): out[0..na) = the na
 // smallest (keep_max=0) or largest (keep_max=1) keys of A U B, ascending.
 // scratch must hold ceil(na/2048)+1 int64 co-ranks.

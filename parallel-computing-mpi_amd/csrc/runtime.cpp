@@ -1091,6 +1091,37 @@ int misort_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64
     return MISORT_OK;
 }
 
+int misort_pass_probe(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, int kind, int hi,
+                      int r, int flip, int reps, float* ms) {
+    if (!c || (dtype != MISORT_U32 && dtype != MISORT_U64) || n <= 0 || !in || !out || in == out || reps < 1 || !ms)
+        return fail(MISORT_E_INVALID, "bad pass_probe arguments");
+    if (kind != misort::KIND_TILE_SORT && kind != misort::KIND_GLOBAL && kind != misort::KIND_SPAN &&
+        kind != misort::KIND_TILE_MERGE)
+        return fail(MISORT_E_INVALID, "bad pass kind");
+    hipStream_t s = c->stream;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    hipError_t err = hipSuccess;
+    auto run = [&](const void* a, void* b) {
+        return dtype == MISORT_U32
+                   ? misort::run_pass<uint32_t>((const uint32_t*)a, (uint32_t*)b, n, kind, hi, r, flip, s)
+                   : misort::run_pass<uint64_t>((const uint64_t*)a, (uint64_t*)b, n, kind, hi, r, flip, s);
+    };
+    err = run(in, out);  // warm-up (and argument check)
+    if (err == hipSuccess) err = hipEventRecord(e0, s);
+    for (int i = 0; i < reps && err == hipSuccess; ++i) err = (i & 1) ? run(out, (void*)in) : run(in, out);
+    if (err == hipSuccess) err = hipEventRecord(e1, s);
+    if (err == hipSuccess) err = hipEventSynchronize(e1);
+    if (err == hipSuccess) err = hipEventElapsedTime(ms, e0, e1);
+    if (err == hipSuccess) *ms /= reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (err == hipErrorInvalidValue) return fail(MISORT_E_INVALID, "pass shape does not fit n");
+    HIPCHK(err);
+    return MISORT_OK;
+}
+
 int misort_parallel_bitonic_sort_oop(misort_ctx* c, int dtype, const void* in, void* out,
                                      int64_t loc, int64_t max_size, void* stream) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");

@@ -26,7 +26,7 @@ U32, U64, F64 = 0, 1, 2
 KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other", "span_pass"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
+_LIB_PATH = os.environ.get("MISORT_LIBRARY") or os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
 _lib = None
 
 
@@ -87,6 +87,7 @@ def lib():
                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_tile_log2": ([i32], i32),
         "misort_plan": ([ctypes.c_int64, i32, ctypes.POINTER(i32), i32], i32),
+        "misort_pass_probe": ([vp, i32, vp, vp, i64, i32, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_float)], i32),
         "misort_group_create": ([i32, ctypes.POINTER(vp)], i32),
         "misort_group_destroy": ([vp], i32),
         "misort_comm_init_group": ([vp, vp, i32], i32),
@@ -385,6 +386,15 @@ class Context:
 
     def profile_reset(self):
         _check(lib().misort_profile_reset(self._h))
+
+    def pass_probe(self, inp, out, kind, hi, r, flip, reps=5, n=None):
+        """Average ms of one HBM pass of a plan shape (tools/pass_costs.py)."""
+        ms = ctypes.c_float()
+        k = KIND_NAMES.index(kind) if isinstance(kind, str) else int(kind)
+        _check(lib().misort_pass_probe(self._h, _dtype_of(inp), _ptr(inp), _ptr(out),
+                                       inp.numel() if n is None else n, k, hi, r, int(flip), reps,
+                                       ctypes.byref(ms)))
+        return ms.value
 
     def profile_read(self):
         """{kind: (launches, total_ms, algorithmic_bytes)}."""
