@@ -832,7 +832,7 @@ void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hi
 // LT: SORT/MERGE tile; LTR: ROWS tile.
 template <typename K, int LT, int LTR>
 hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                         LaunchHook* hook) {
+                         LaunchHook* hook, const StageIO* io) {
     const PlanKnobs& kn = plan_knobs();
     const std::vector<Pass> ps = plan_for<K, LT, LTR>(n);
     const int np = (int)ps.size();
@@ -844,7 +844,22 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
-        launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s);
+        const bool contig = p.kind == KIND_TILE_SORT || p.kind == KIND_TILE_MERGE;
+        const bool cin = io && io->before_first && i == 0;
+        const bool cout = io && io->after_last && i == np - 1 && contig;
+        if (cin || cout) {
+            // chunk by chunk (contiguous tiles only: offsets keep the tile grid)
+            const int64_t ch = io->chunk;
+            if (ch <= 0 || (ch & ((1 << LT) - 1)) || !contig) return hipErrorInvalidValue;
+            for (int64_t k0 = 0; k0 < n; k0 += ch) {
+                const int64_t k1 = n - k0 < ch ? n : k0 + ch;
+                if (cin && io->before_first(k0, k1, s)) return hipErrorUnknown;
+                launch_pass<K, LT, LTR>(src + k0, dst + k0, k1 - k0, p, ord_in, s);
+                if (cout && io->after_last(k0, k1, s)) return hipErrorUnknown;
+            }
+        } else {
+            launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s);
+        }
         src = dst;
     }
     return hipGetLastError();
@@ -855,15 +870,15 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
 // Definition shared by sort_u32.hip / sort_u64.hip (one explicit instantiation each).
 template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                      LaunchHook* hook) {
+                      LaunchHook* hook, const StageIO* io) {
     if (n <= 0) return hipSuccess;
     if (sizeof(K) == 4 && ord_in) return hipErrorInvalidValue;
     constexpr int S = KT<K>::LT_SMALL;  // 14 (u32) / 13 (u64): the 64 KiB tile
     const PlanKnobs& kn = plan_knobs();
     const bool big = kn.tile_u32 == 15, rbig = kn.rows_tile_u32 == 15;
-    if (big && rbig) return local_sort_lt<K, S + 1, S + 1>(in, out, n, ord_in, scratch, s, hook);
-    if (big) return local_sort_lt<K, S + 1, S>(in, out, n, ord_in, scratch, s, hook);
-    return local_sort_lt<K, S, S>(in, out, n, ord_in, scratch, s, hook);
+    if (big && rbig) return local_sort_lt<K, S + 1, S + 1>(in, out, n, ord_in, scratch, s, hook, io);
+    if (big) return local_sort_lt<K, S + 1, S>(in, out, n, ord_in, scratch, s, hook, io);
+    return local_sort_lt<K, S, S>(in, out, n, ord_in, scratch, s, hook, io);
 }
 
 // One pass of any shape (pass-cost probes, tools/pass_costs.py).

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
+
 namespace misort {
 
 // Kernel families, used for per-launch profiling (HIP events) and reporting.
@@ -26,6 +28,19 @@ struct LaunchHook {
     virtual ~LaunchHook() = default;
 };
 
+// Chunked first/last pass of a local sort, for host staging that overlaps the
+// PCIe copies with the sort (misort_sort_host).  The SORT pass runs chunk by
+// chunk; before chunk [k0, k1) is read, before_first(k0, k1, s) makes stream s
+// wait for those input keys.  If after_last is set, the final pass (a
+// contiguous-tile MERGE or SORT pass) also runs chunk by chunk and
+// after_last(k0, k1, s) is called once output keys [k0, k1) are enqueued.
+// `chunk` is a multiple of the SORT tile.
+struct StageIO {
+    int64_t chunk = 0;
+    std::function<int(int64_t, int64_t, hipStream_t)> before_first;
+    std::function<int(int64_t, int64_t, hipStream_t)> after_last;
+};
+
 // Local ascending sort of n keys: in -> out (in == out allowed).
 // K = uint32_t or uint64_t.  ord_in: the input holds IEEE doubles that are
 // mapped to order-preserving u64 on load (K must be uint64_t); the output
@@ -34,7 +49,7 @@ struct LaunchHook {
 // rewriting `out` in place (copy-shaped HBM traffic).
 template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                      LaunchHook* hook);
+                      LaunchHook* hook, const StageIO* io = nullptr);
 
 // One HBM pass of the given shape (kind KIND_TILE_SORT / KIND_GLOBAL /
 // KIND_SPAN / KIND_TILE_MERGE, hi, R, flip as in the plan) over n keys: the

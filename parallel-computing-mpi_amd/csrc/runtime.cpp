@@ -20,6 +20,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -396,13 +397,28 @@ struct misort_ctx {
     DevBuf qa, qb, qcnt;  // quick sort: current run, merge target, exchanged counts
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // host staging (misort_sort_host): device keys, pinned ring, copy stream
+    DevBuf host_keys;
+    static constexpr int RING = 3;
+    void* ring[RING] = {};
+    size_t ring_bytes = 0;
+    hipEvent_t ring_ev[RING] = {};
+    bool ring_busy[RING] = {};
+    hipStream_t copy_stream = nullptr;
     Profiler prof;
     int64_t xchg_bytes = 0, xchg_stages = 0, xchg_full_bytes = 0;
     bool full_exchange = getenv("MISORT_FULL_EXCHANGE") != nullptr;
     // relay compare-split exchanges through the other GPUs (P > 2): MISORT_RELAY=0 disables
     bool relay = !getenv("MISORT_RELAY") || atoi(getenv("MISORT_RELAY")) != 0;
     DevBuf relay_buf;
-    ~misort_ctx() { delete tr; }
+    ~misort_ctx() {
+        delete tr;
+        for (int i = 0; i < RING; ++i) {
+            if (ring[i]) (void)hipHostFree(ring[i]);
+            if (ring_ev[i]) (void)hipEventDestroy(ring_ev[i]);
+        }
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    }
 };
 
 namespace {
@@ -411,17 +427,17 @@ hipStream_t pick(misort_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream
 misort::LaunchHook* hook(misort_ctx* c) { return c->prof.on ? &c->prof : nullptr; }
 
 int do_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, bool ord_in,
-                  hipStream_t s) {
+                  hipStream_t s, const misort::StageIO* io = nullptr) {
     // scratch for the ping-pong passes (grown on demand, kept for the context)
     int rc = c->pong.ensure(std::max<size_t>(16, (size_t)n * key_bytes(dtype)));
     if (rc) return rc;
     hipError_t e;
     if (dtype == MISORT_U32)
         e = misort::local_sort<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, false, (uint32_t*)c->pong.p, s,
-                                         hook(c));
+                                         hook(c), io);
     else
         e = misort::local_sort<uint64_t>((const uint64_t*)in, (uint64_t*)out, n, ord_in, (uint64_t*)c->pong.p, s,
-                                         hook(c));
+                                         hook(c), io);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "local_sort: %s", hipGetErrorString(e));
     return MISORT_OK;
 }
@@ -531,8 +547,11 @@ int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sb
     return c->tr->group_p2p(r2, s);
 }
 
+// io: optional chunked first/last pass (host staging).  Its after_last hook is
+// used only when no exchange stage follows the local sort (P = 1); it then also
+// owns the f64 back-conversion of each output chunk.
 int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
-                  int64_t max_size, hipStream_t s) {
+                  int64_t max_size, hipStream_t s, const misort::StageIO* io = nullptr) {
     if (!valid_dtype(dtype)) return fail(MISORT_E_INVALID, "bad dtype %d", dtype);
     if (loc < 0 || max_size < loc) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld",
                                                (long long)loc, (long long)max_size);
@@ -564,7 +583,14 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     }
     // The local sort writes where the stage parity leaves the result in `out`.
     void* cur = (nst & 1) ? work : out;
-    if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s))) return rc;
+    misort::StageIO lio;
+    const bool chunk_out = io && io->after_last && nst == 0;
+    if (io) {
+        lio = *io;
+        if (!chunk_out) lio.after_last = nullptr;
+    }
+    if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s, io ? &lio : nullptr))) return rc;
+    if (chunk_out) return MISORT_OK;
     void* other = (cur == work) ? out : work;
     for (int st = 0; st < nst; ++st) {
         const int q = partner[st];
@@ -1227,27 +1253,160 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     return MISORT_OK;
 }
 
+// Host staging: keys travel host <-> HBM in chunks through a ring of pinned
+// buffers, overlapped with the sort:
+//   in:  host memcpy of chunk i into a pinned slot (several threads) | DMA of
+//        chunk i-1 on the copy stream | SORT pass of chunk i-2 on the sort
+//        stream (tile-local, so it starts as soon as its chunk has landed);
+//   out: (P = 1) the final MERGE pass and the f64 back-conversion run chunk by
+//        chunk, each chunk's D2H and host copy overlapping the next chunk;
+//        (P > 1) chunked D2H after the last compare-split.
+// MISORT_STAGE_CHUNK sets the chunk (keys, rounded to the tile; default 2^24).
+namespace {
+
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    static const int T = [] {
+        const char* e = getenv("MISORT_STAGE_THREADS");
+        int t = e ? atoi(e) : 8;
+        return t < 1 ? 1 : t > 64 ? 64 : t;
+    }();
+    const size_t MIN = (size_t)4 << 20;  // below this, one thread
+    if (T == 1 || bytes < 2 * MIN) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    int t = (int)std::min<size_t>((size_t)T, bytes / MIN);
+    const size_t part = (bytes / t + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int i = 1; i < t; ++i) {
+        const size_t o = (size_t)i * part;
+        if (o >= bytes) break;
+        th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
+    }
+    memcpy(dst, src, std::min(part, bytes));
+    for (auto& x : th) x.join();
+}
+
+int64_t stage_chunk(int dtype) {
+    const char* e = getenv("MISORT_STAGE_CHUNK");
+    int64_t ch = e ? atoll(e) : ((int64_t)1 << 24);
+    const int64_t tile = (int64_t)1 << misort::tile_log2((int)key_bytes(dtype));
+    if (ch < tile) ch = tile;
+    return (ch + tile - 1) / tile * tile;
+}
+
+int ring_ensure(misort_ctx* c, size_t bytes) {
+    if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < misort_ctx::RING; ++i) {
+        if (!c->ring_ev[i]) HIPCHK(hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming));
+        c->ring_busy[i] = false;
+    }
+    if (bytes <= c->ring_bytes) return MISORT_OK;
+    for (int i = 0; i < misort_ctx::RING; ++i) {
+        if (c->ring[i]) HIPCHK(hipHostFree(c->ring[i]));
+        c->ring[i] = nullptr;
+    }
+    c->ring_bytes = 0;
+    for (int i = 0; i < misort_ctx::RING; ++i) HIPCHK(hipHostMalloc(&c->ring[i], bytes, hipHostMallocDefault));
+    c->ring_bytes = bytes;
+    return MISORT_OK;
+}
+
+// Output side: chunk [k0, k1) of dev (ready in stream order on `s`) -> host.
+struct OutPipe {
+    misort_ctx* c;
+    const char* dev;
+    char* host;
+    size_t w;
+    int next = 0;
+    int64_t pend_k0[misort_ctx::RING] = {}, pend_k1[misort_ctx::RING] = {};
+    int drain(int slot) {
+        if (!c->ring_busy[slot]) return MISORT_OK;
+        HIPCHK(hipEventSynchronize(c->ring_ev[slot]));
+        par_memcpy(host + pend_k0[slot] * w, c->ring[slot], (size_t)(pend_k1[slot] - pend_k0[slot]) * w);
+        c->ring_busy[slot] = false;
+        return MISORT_OK;
+    }
+    int push(int64_t k0, int64_t k1, hipStream_t s) {
+        const int slot = next;
+        next = (next + 1) % misort_ctx::RING;
+        int rc = drain(slot);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(c->ring[slot], dev + k0 * w, (size_t)(k1 - k0) * w, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(c->ring_ev[slot], s));
+        c->ring_busy[slot] = true;
+        pend_k0[slot] = k0;
+        pend_k1[slot] = k1;
+        return MISORT_OK;
+    }
+    int finish() {
+        for (int i = 0; i < misort_ctx::RING; ++i) {
+            const int slot = (next + i) % misort_ctx::RING;
+            int rc = drain(slot);
+            if (rc) return rc;
+        }
+        return MISORT_OK;
+    }
+};
+
+}  // namespace
+
 int misort_sort_host(misort_ctx* c, int dtype, const void* h_in, void* h_out, int64_t loc,
                      int64_t max_size) {
     if (!c || !valid_dtype(dtype) || loc < 0 || (loc > 0 && (!h_in || !h_out)))
         return fail(MISORT_E_INVALID, "bad sort_host arguments");
-    const size_t bytes = (size_t)loc * key_bytes(dtype);
-    if (bytes > c->pinned_bytes) {
-        if (c->pinned) HIPCHK(hipHostFree(c->pinned));
-        c->pinned = nullptr;
-        c->pinned_bytes = 0;
-        HIPCHK(hipHostMalloc(&c->pinned, std::max<size_t>(bytes, 64), hipHostMallocDefault));
-        c->pinned_bytes = std::max<size_t>(bytes, 64);
-    }
-    DevBuf dev;
-    int rc = dev.ensure(std::max<size_t>(bytes, 64));
+    if (loc > max_size) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld", (long long)loc,
+                                    (long long)max_size);
+    const size_t w = key_bytes(dtype);
+    const int64_t ch = stage_chunk(dtype);
+    int rc = c->host_keys.ensure(std::max<size_t>((size_t)std::max<int64_t>(loc, 1) * w, 64));
     if (rc) return rc;
-    memcpy(c->pinned, h_in, bytes);
-    HIPCHK(hipMemcpyAsync(dev.p, c->pinned, bytes, hipMemcpyHostToDevice, c->stream));
-    if ((rc = parallel_sort(c, dtype, dev.p, dev.p, loc, max_size, c->stream))) return rc;
-    HIPCHK(hipMemcpyAsync(c->pinned, dev.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    memcpy(h_out, c->pinned, bytes);
+    if ((rc = ring_ensure(c, (size_t)std::min<int64_t>(std::max<int64_t>(loc, 1), ch) * w))) return rc;
+    char* dev = (char*)c->host_keys.p;
+    hipStream_t s = c->stream, cs = c->copy_stream;
+    int in_next = 0;
+    misort::StageIO io;
+    io.chunk = ch;
+    io.before_first = [&](int64_t k0, int64_t k1, hipStream_t st) -> int {
+        const int slot = in_next;
+        in_next = (in_next + 1) % misort_ctx::RING;
+        if (c->ring_busy[slot]) HIPCHK(hipEventSynchronize(c->ring_ev[slot]));
+        const size_t bytes = (size_t)(k1 - k0) * w;
+        par_memcpy(c->ring[slot], (const char*)h_in + k0 * w, bytes);
+        HIPCHK(hipMemcpyAsync(dev + k0 * w, c->ring[slot], bytes, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipEventRecord(c->ring_ev[slot], cs));
+        c->ring_busy[slot] = true;
+        HIPCHK(hipStreamWaitEvent(st, c->ring_ev[slot], 0));
+        return MISORT_OK;
+    };
+    OutPipe op{c, dev, (char*)h_out, w};
+    bool staged_out = false;
+    io.after_last = [&](int64_t k0, int64_t k1, hipStream_t st) -> int {
+        if (!staged_out) {  // the input side is done with the ring
+            for (int i = 0; i < misort_ctx::RING; ++i)
+                if (c->ring_busy[i]) {
+                    HIPCHK(hipEventSynchronize(c->ring_ev[i]));
+                    c->ring_busy[i] = false;
+                }
+            staged_out = true;
+        }
+        if (dtype == MISORT_F64) HIPCHK(misort::ord_to_f64((uint64_t*)(dev + k0 * w), k1 - k0, st));
+        return op.push(k0, k1, st);
+    };
+    if (loc == 0) return parallel_sort(c, dtype, dev, dev, 0, max_size, s);
+    if ((rc = parallel_sort(c, dtype, dev, dev, loc, max_size, s, &io))) return rc;
+    if (!staged_out) {
+        // P > 1 (or a plan whose last pass is not contiguous): chunked D2H now
+        for (int i = 0; i < misort_ctx::RING; ++i)
+            if (c->ring_busy[i]) {
+                HIPCHK(hipEventSynchronize(c->ring_ev[i]));
+                c->ring_busy[i] = false;
+            }
+        for (int64_t k0 = 0; k0 < loc; k0 += ch)
+            if ((rc = op.push(k0, std::min(loc, k0 + ch), s))) return rc;
+    }
+    if ((rc = op.finish())) return rc;
+    HIPCHK(hipStreamSynchronize(s));
     return MISORT_OK;
 }
 

@@ -342,13 +342,17 @@ class Context:
                                        ctypes.byref(err), self._stream(stream)))
         return int(err.value)
 
-    def sort_host(self, arr, max_size=None):
-        """numpy block -> pinned staging -> GPU parallel sort -> numpy."""
+    def sort_host(self, arr, max_size=None, out=None):
+        """numpy block -> pinned staging ring -> GPU parallel sort -> numpy
+        (chunked and overlapped; `out` may be a preallocated array)."""
         import numpy as np
         arr = np.ascontiguousarray(arr)
         dt = {np.dtype(np.uint32): U32, np.dtype(np.uint64): U64,
               np.dtype(np.float64): F64}[arr.dtype]
-        out = np.empty_like(arr)
+        if out is None:
+            out = np.empty_like(arr)
+        elif out.dtype != arr.dtype or out.size < arr.size or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous array of the input dtype and size")
         mx = arr.size if max_size is None else int(max_size)
         _check(lib().misort_sort_host(self._h, dt, arr.ctypes.data_as(ctypes.c_void_p),
                                       out.ctypes.data_as(ctypes.c_void_p), arr.size, mx))

@@ -1,0 +1,104 @@
+"""Host staging (misort_sort_host): keys travel host <-> HBM
+in chunks through a pinned ring, the SORT pass runs per chunk as its keys land
+and (P = 1) the final pass + D2H run per chunk.  Small MISORT_STAGE_CHUNK
+values force many chunks, a ragged last chunk and ring wrap-around; results
+must equal the oracle / the golden fixtures bit for bit."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+torch = pytest.importorskip("torch")
+import misort  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLD_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+with open(os.path.join(GOLD_DIR, "golden.json")) as f:
+    GOLD = json.load(f)["cases"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = misort.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def chunk(monkeypatch):
+    def set_chunk(keys):
+        monkeypatch.setenv("MISORT_STAGE_CHUNK", str(keys))
+    return set_chunk
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("n", [1, 5, 32768, 32769, 100003, 1 << 20, 3000017])
+@pytest.mark.parametrize("ch", [1 << 15, 1 << 17])
+def test_staged_u32(ctx, chunk, n, ch):
+    chunk(ch)
+    x = O.splitmix(0x5EED0001 + n, n, np.uint32)
+    np.testing.assert_array_equal(ctx.sort_host(x), np.sort(x))
+
+
+@pytest.mark.parametrize("n", [7, 16384, 50021, 1 << 19])
+def test_staged_u64_mix(ctx, chunk, n):
+    chunk(1 << 14)
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 2**64 - 1, size=n, dtype=np.uint64, endpoint=True)
+    x[::3] = rng.integers(0, 1024, size=x[::3].size).astype(np.uint64)  # duplicate-heavy
+    x[::11] = np.uint64(2**64 - 1)  # sentinel collisions
+    x[::13] = 0
+    np.testing.assert_array_equal(ctx.sort_host(x), np.sort(x))
+
+
+@pytest.mark.parametrize("n", [13, 1031, 300007])
+def test_staged_f64_reference_generator(ctx, chunk, n):
+    chunk(1 << 14)
+    x = O.generate_f64(n)  # psort.cc:587-614
+    y = ctx.sort_host(x)
+    np.testing.assert_array_equal(y.view(np.uint64), O.local_sort(x).view(np.uint64))
+
+
+def test_staged_default_chunk_large(ctx, chunk):
+    chunk(1 << 24)
+    n = (1 << 26) + 12345  # 5 chunks of the default size, ragged tail
+    x = O.splitmix(0x5EED0002, n, np.uint32)
+    y = ctx.sort_host(x)
+    assert np.all(y[1:] >= y[:-1])
+    assert int(x.astype(np.uint64).sum()) == int(y.astype(np.uint64).sum())
+    np.testing.assert_array_equal(np.bincount(x >> 20, minlength=4096), np.bincount(y >> 20, minlength=4096))
+
+
+PSORT = [c for c in GOLD if c["mode"] == "psort" and c["p"] > 1 and c["n"] >= 1000
+         and c.get("algo", "bitonic") == "bitonic"]
+
+
+@pytest.mark.parametrize("case", PSORT, ids=lambda c: f"N{c['n']}_P{c['p']}")
+def test_staged_group_golden(case, monkeypatch):
+    """P ranks (threads, one context each): chunked input, exchange stages,
+    chunked D2H; the concatenated blocks equal the reference's output."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("MISORT_STAGE_CHUNK", str(1 << 14))
+    n, p = case["n"], case["p"]
+    x = O.generate_f64(n)
+    sizes = misort.block_sizes(n, p)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    blocks = [np.ascontiguousarray(x[offs[r]:offs[r + 1]]) for r in range(p)]
+    g = misort.Group(p)
+    try:
+        res = g.run(lambda r, c: c.sort_host(blocks[r], max_size=n // p + 1))
+    finally:
+        g.close()
+    y = np.concatenate(res)
+    assert sha(y) == case["out_sha256"]
