@@ -325,6 +325,140 @@ __device__ __forceinline__ void sort_levels(K* s, int t) {
     }
 }
 
+// ------------------------------------------------ in-wave tile sort (u32)
+//
+// The SORT pass for u32 keys keeps each wave's 2^11 keys in registers for
+// levels 1..11: lane l of wave w holds the 32 consecutive keys
+// v = (w << 11) | (l << 5) | c, c = register.  Stages on c run in registers;
+// stages on the lane bits (virtual bits 5..10) exchange between lanes without
+// LDS -- DPP (quad_perm, row_shl/shr with bank masks, row_mirror,
+// row_half_mirror) within a 16-lane row, v_permlane16/32_swap across rows --
+// and the element whose top compared bit is 0 keeps the minimum through one
+// v_med3_u32 (med3(x, p, 0) = min, med3(x, p, ~0) = max).  With
+// MISORT_WAVE_LEVELS = 11, levels 12..15 do their wave-bit strides
+// (2^14..2^11) in one LDS phase each and return to the register layout (10 LDS
+// round trips per tile instead of 27) -- but the cross-lane ops are VALU-heavy
+// (DPP hazards, two DPPs for xor 4/8, permlane swaps): measured per 2^30 SORT
+// pass 6.9 ms (in the wave up to level 11), 5.23 (7), 5.16 (8), 5.21 (9),
+// 5.57 ms (all LDS; profiles/r01/ab/wave_levels.txt).  Default: levels 6..8 in
+// the wave (quad_perm / row_half_mirror only), 9..15 in LDS phases.
+// (Semantics of every cross-lane op: tools/dpp_probe.hip.)
+#ifndef MISORT_WAVE_SORT
+#define MISORT_WAVE_SORT 1
+#endif
+// highest level run in the wave (6..11); the levels above go through LDS phases
+#ifndef MISORT_WAVE_LEVELS
+#define MISORT_WAVE_LEVELS 8
+#endif
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+    return max(min(a, b), min(max(a, b), c));  // v_med3_u32
+}
+
+template <int CTRL, int BANK>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, BANK, false);
+}
+// all lanes written: no `old` operand to materialise
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_all(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
+// Value of v in lane (lane ^ X), X in {1,2,3,4,7,8,15,16,31,32,63}.
+template <int X>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, int lane) {
+    if constexpr (X == 1) return dpp_all<0xB1>(v);        // quad_perm [1,0,3,2]
+    else if constexpr (X == 2) return dpp_all<0x4E>(v);   // quad_perm [2,3,0,1]
+    else if constexpr (X == 3) return dpp_all<0x1B>(v);   // quad_perm [3,2,1,0]
+    else if constexpr (X == 7) return dpp_all<0x141>(v);  // row_half_mirror
+    else if constexpr (X == 15) return dpp_all<0x140>(v); // row_mirror
+    else if constexpr (X == 4) return dpp<0x114, 0xA>(dpp<0x104, 0x5>(v, v), v);  // row_shl/shr:4
+    else if constexpr (X == 8) return dpp<0x118, 0xC>(dpp<0x108, 0x3>(v, v), v);  // row_shl/shr:8
+    else if constexpr (X == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (X == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    } else if constexpr (X == 31) return lane_xor<16>(lane_xor<15>(v, lane), lane);
+    else return lane_xor<32>(lane_xor<31>(v, lane), lane);  // X == 63
+}
+
+// Flip of level m (6..11): v <-> v ^ (2^m - 1) = register c <-> 31-c, lane ^ (2^(m-5)-1).
+template <int M>
+__device__ __forceinline__ void wave_flip(uint32_t (&x)[32], int lane) {
+    constexpr int X = (1 << (M - 5)) - 1;
+    const uint32_t bnd = ((lane >> (M - 6)) & 1) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const uint32_t pa = lane_xor<X>(x[31 - c], lane), pb = lane_xor<X>(x[c], lane);
+        x[c] = med3u(x[c], pa, bnd);
+        x[31 - c] = med3u(x[31 - c], pb, bnd);
+    }
+}
+
+// Half-cleaner on lane bit J (virtual bit 5+J).
+template <int J>
+__device__ __forceinline__ void wave_half(uint32_t (&x)[32], int lane) {
+    if constexpr (J >= 4) {
+        // rows apart: v_permlane{16,32}_swap pairs registers (c, c+16) so that
+        // every lane holds (lower, upper) of one pair; compare; swap back
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            auto r = J == 4 ? __builtin_amdgcn_permlane16_swap(x[c], x[c + 16], false, false)
+                            : __builtin_amdgcn_permlane32_swap(x[c], x[c + 16], false, false);
+            uint32_t lo = min(r[0], r[1]), hi = max(r[0], r[1]);
+            auto b = J == 4 ? __builtin_amdgcn_permlane16_swap(lo, hi, false, false)
+                            : __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+            x[c] = b[0];
+            x[c + 16] = b[1];
+        }
+    } else {
+        const uint32_t bnd = ((lane >> J) & 1) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) x[c] = med3u(x[c], lane_xor<(1 << J)>(x[c], lane), bnd);
+    }
+}
+
+// Half-cleaners on lane bits J..0, then the register bits 4..0.
+template <int J>
+__device__ __forceinline__ void wave_halves(uint32_t (&x)[32], int lane) {
+    if constexpr (J >= 0) {
+        wave_half<J>(x, lane);
+        wave_halves<J - 1>(x, lane);
+    } else {
+        reg_stages_c<uint32_t, 4, 5, false>(x);
+    }
+}
+
+// Levels M..TOP (<= 11) entirely in the wave.
+template <int M, int TOP>
+__device__ __forceinline__ void wave_levels(uint32_t (&x)[32], int lane) {
+    if constexpr (M <= TOP) {
+        wave_flip<M>(x, lane);
+        wave_halves<M - 7>(x, lane);
+        wave_levels<M + 1, TOP>(x, lane);
+    }
+}
+
+// Levels M..LT: wave-bit strides in one LDS phase (window [10,15)), the rest in the wave.
+template <int M, int LT>
+__device__ __forceinline__ void wave_big_levels(uint32_t* s, uint32_t (&x)[32], int t) {
+    if constexpr (M <= LT) {
+        const int a0 = pad(t << 5);
+#pragma unroll
+        for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
+        __syncthreads();
+        phase_c<uint32_t, 10, M - 11, M - 11, true>(s, t);
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
+        wave_halves<5>(x, t & 63);
+        wave_big_levels<M + 1, LT>(s, x, t);
+    }
+}
+
 // Stages on the slot bits of register-held vectors: relative slot bits
 // TOP..TOP-CNT+1, the first one a flip if FLIP (the flip complements every
 // slot bit; mirrored upper slots complete it to the tile's own v <-> ~v).
@@ -562,7 +696,33 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
             __syncthreads();
             const int64_t nxt = tile + gridDim.x;
             if (PERSIST && nxt < m.ntiles) tile_fetch<K, LT, MODE, SL, P.MLOAD, ORD>(pre, in, m, nxt, n, t);
-            if constexpr (MODE == TM_SORT) {
+            if constexpr (MODE == TM_SORT && MISORT_WAVE_SORT && sizeof(K) == 4 && LT == 15) {
+                // levels 1..11 in the wave, 12..15 with one LDS phase each
+                uint32_t x[32];
+                const int a0 = pad(t << 5);
+#pragma unroll
+                for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
+                reg_stages_c<uint32_t, 0, 1, true>(x);
+                reg_stages_c<uint32_t, 1, 2, true>(x);
+                reg_stages_c<uint32_t, 2, 3, true>(x);
+                reg_stages_c<uint32_t, 3, 4, true>(x);
+                reg_stages_c<uint32_t, 4, 5, true>(x);
+                constexpr int WL = MISORT_WAVE_LEVELS;
+                wave_levels<6, WL>(x, t & 63);
+                if constexpr (WL >= 11) {
+                    __syncthreads();  // every wave has read its keys: the LDS tile is free
+                    wave_big_levels<12, LT>((uint32_t*)s, x, t);
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
+                    __syncthreads();
+                } else {
+                    // each lane rewrites only the keys it read: no barrier before
+#pragma unroll
+                    for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
+                    __syncthreads();
+                    sort_levels<K, WL + 1, LT>(s, t);
+                }
+            } else if constexpr (MODE == TM_SORT) {
                 {   // levels 1..5: window [0,5), 32 consecutive keys per lane
                     K v[32];
                     const int a0 = pad(t << 5);
