@@ -180,6 +180,25 @@ int misort_set_full_exchange(misort_ctx* ctx, int on);
  * over the pair's own xGMI link, P-2 take two hops through the other GPUs, so
  * all P-1 links of every GPU carry the stage.  Bytes delivered are identical. */
 int misort_set_relay(misort_ctx* ctx, int on);
+
+/* Delta-code the keys of each compare-split message (default on; env
+ * MISORT_COMPRESS=0 turns it off).  The k keys one side sends are a sorted
+ * run: blocks of 1024 keys travel as first key + gaps packed at the block's
+ * bit width (lossless; ~4x smaller for 2^27 uniform u32 keys per rank).  A
+ * side whose coded message would not be smaller sends it raw; the receiver
+ * tells them apart by size.  Replaces the raw MPI_Sendrecv payload of
+ * psort.cc:122-123 / 146-147; the kept keys are unchanged. */
+int misort_set_compress(misort_ctx* ctx, int on);
+
+/* Tooling: encode a sorted device run of n keys with the exchange codec,
+ * then decode it (into `decoded` if non-null); average ms of each over
+ * `reps` launches (HIP events) and the coded size in bytes. */
+int misort_codec_probe(misort_ctx* ctx, int dtype, const void* keys, int64_t n, int reps, float* enc_ms,
+                       float* dec_ms, int64_t* coded_bytes, void* decoded);
+
+/* Bytes the exchanges since the last call would have moved uncoded (sent +
+ * received; the coded bytes are misort_exchange_stats' `bytes`).  Resets. */
+int misort_exchange_raw_bytes(misort_ctx* ctx, int64_t* raw_bytes);
 /* Host logic of the bracketed exchange (pure functions, no GPU):
  * samples of a sorted block of n keys are keys[min(c*S, n-1)], c = 0..count-1,
  * S = misort_sample_stride(n), count = misort_sample_count(n).

@@ -99,6 +99,20 @@ hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s);
 hipError_t fill_splitmix_u32(uint32_t* out, int64_t n, uint64_t seed, int64_t g0, hipStream_t s);
 hipError_t fill_splitmix_u64(uint64_t* out, int64_t n, uint64_t seed, int64_t g0, hipStream_t s);
 
+// Lossless delta coding of a sorted run (codec.hip), for the compare-split
+// exchange: blocks of 1024 keys, first key + gaps packed at the block's width.
+// codec_encode writes the stream to `out` (<= codec_max_words(n) u32 words)
+// and its length in words to *d_total (device); scratch holds
+// codec_scratch_bytes(n) bytes.  codec_decode restores the n keys.
+int64_t codec_blocks(int64_t n);
+size_t codec_scratch_bytes(int64_t n);
+int64_t codec_max_words(int64_t n, int key_bytes);
+template <typename K>
+hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, size_t scratch_bytes,
+                        uint32_t* d_total, hipStream_t s);
+template <typename K>
+hipError_t codec_decode(const uint32_t* in, int64_t n, K* keys, hipStream_t s);
+
 // Tile geometry per key type (exported for documentation/tests).
 int tile_log2(int key_bytes);
 

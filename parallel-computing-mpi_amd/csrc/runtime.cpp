@@ -411,6 +411,10 @@ struct misort_ctx {
     // relay compare-split exchanges through the other GPUs (P > 2): MISORT_RELAY=0 disables
     bool relay = !getenv("MISORT_RELAY") || atoi(getenv("MISORT_RELAY")) != 0;
     DevBuf relay_buf;
+    // delta-coded exchange (codec.hip): MISORT_COMPRESS=0 / misort_set_compress(ctx, 0) disables
+    bool compress = !getenv("MISORT_COMPRESS") || atoi(getenv("MISORT_COMPRESS")) != 0;
+    DevBuf enc_send, enc_recv, codec_scr;
+    int64_t xchg_raw_bytes = 0;  // what the coded stages would have moved uncoded
     ~misort_ctx() {
         delete tr;
         for (int i = 0; i < RING; ++i) {
@@ -493,13 +497,18 @@ int64_t corank_lower(const std::vector<T>& sa, int64_t na, const std::vector<T>&
 // direct time (4x less at P = 8).  All ranks take part, including those whose
 // own message is empty, because they relay for the others.
 int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sbytes, void* rbuf, size_t rbytes,
-                   hipStream_t s) {
+                   hipStream_t s, size_t* rbytes_out = nullptr) {
     const int P = c->nranks, me = c->rank, pm = me ^ (1 << bit);
     int rc;
-    std::vector<int64_t> m;  // keys each rank sends to its partner
+    std::vector<int64_t> m;  // units (w bytes) each rank sends to its partner
     const int64_t mine = (int64_t)(sbytes / w);
     if ((rc = c->tr->allgather_i64(&mine, 1, m, s))) return rc;
-    if ((size_t)m[pm] * w != rbytes) return fail(MISORT_E_INVALID, "relay: partner size mismatch");
+    if (rbytes_out) {  // the partner's size is learnt here; rbytes is the capacity
+        if ((size_t)m[pm] * w > rbytes) return fail(MISORT_E_CAPACITY, "relay: partner message exceeds buffer");
+        *rbytes_out = (size_t)m[pm] * w;
+    } else if ((size_t)m[pm] * w != rbytes) {
+        return fail(MISORT_E_INVALID, "relay: partner size mismatch");
+    }
     auto bnd = [&](int x, int i) { return (int64_t)((__int128)i * m[x] / P); };
     auto rel = [&](int x) {  // relays of x's pair, ascending
         std::vector<int> r;
@@ -545,6 +554,61 @@ int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sb
     }
     if ((rc = c->tr->group_p2p(r1, s))) return rc;
     return c->tr->group_p2p(r2, s);
+}
+
+// One compare-split message exchange of k sorted keys each way, delta-coded
+// (codec.hip).  *rkeys receives the partner's k keys (decoded into c->recv, or
+// the raw message in c->enc_recv when the partner sent it uncoded).
+int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sbuf, int64_t k, const void** rkeys,
+                   hipStream_t s) {
+    const size_t w = key_bytes(dtype);
+    const int64_t raw_words = k * (int64_t)w / 4, maxw = misort::codec_max_words(k, (int)w);
+    int rc;
+    if ((rc = c->enc_send.ensure((size_t)maxw * 4))) return rc;
+    if ((rc = c->enc_recv.ensure((size_t)std::max(maxw, raw_words) * 4))) return rc;
+    const size_t scr = misort::codec_scratch_bytes(k) + 64;
+    if ((rc = c->codec_scr.ensure(scr))) return rc;
+    if ((rc = c->small.ensure(64))) return rc;
+    uint32_t* d_total = (uint32_t*)c->small.p;
+    hipError_t e = w == 4 ? misort::codec_encode<uint32_t>((const uint32_t*)sbuf, k, (uint32_t*)c->enc_send.p,
+                                                           c->codec_scr.p, scr, d_total, s)
+                          : misort::codec_encode<uint64_t>((const uint64_t*)sbuf, k, (uint32_t*)c->enc_send.p,
+                                                           c->codec_scr.p, scr, d_total, s);
+    if (e != hipSuccess) return fail(MISORT_E_HIP, "codec_encode: %s", hipGetErrorString(e));
+    uint32_t coded = 0;
+    HIPCHK(hipMemcpyAsync(&coded, d_total, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const bool use = (int64_t)coded < raw_words;
+    const void* msg = use ? c->enc_send.p : sbuf;
+    const size_t mbytes = use ? (size_t)coded * 4 : (size_t)k * w;
+    size_t rb = 0;
+    if (relayed) {
+        rc = relay_exchange(c, 4, ilog2(q ^ c->rank), msg, mbytes, c->enc_recv.p, c->enc_recv.bytes, s, &rb);
+    } else {
+        // sizes first (8 bytes), then the messages
+        int64_t* d_sz = (int64_t*)c->small.p + 2;
+        const int64_t mine = (int64_t)mbytes;
+        int64_t theirs = 0;
+        HIPCHK(hipMemcpyAsync(d_sz, &mine, 8, hipMemcpyHostToDevice, s));
+        if ((rc = c->tr->sendrecv(d_sz, 8, d_sz + 1, 8, q, s))) return rc;
+        HIPCHK(hipMemcpyAsync(&theirs, d_sz + 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (theirs < 0 || (size_t)theirs > c->enc_recv.bytes) return fail(MISORT_E_CAPACITY, "coded message size");
+        rb = (size_t)theirs;
+        rc = c->tr->sendrecv(msg, mbytes, c->enc_recv.p, rb, q, s);
+    }
+    if (rc) return rc;
+    c->xchg_bytes += (int64_t)(mbytes + rb);
+    c->xchg_raw_bytes += (int64_t)(2 * k * w);
+    if ((int64_t)rb >= raw_words * 4) {  // sent uncoded
+        *rkeys = c->enc_recv.p;
+        return MISORT_OK;
+    }
+    e = w == 4 ? misort::codec_decode<uint32_t>((const uint32_t*)c->enc_recv.p, k, (uint32_t*)c->recv.p, s)
+               : misort::codec_decode<uint64_t>((const uint32_t*)c->enc_recv.p, k, (uint64_t*)c->recv.p, s);
+    if (e != hipSuccess) return fail(MISORT_E_HIP, "codec_decode: %s", hipGetErrorString(e));
+    *rkeys = c->recv.p;
+    return MISORT_OK;
 }
 
 // io: optional chunked first/last pass (host staging).  Its after_last hook is
@@ -630,7 +694,8 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         c->xchg_full_bytes += (int64_t)((loc + nq) * w);
         const bool relayed = c->relay && p > 2;
         if (k == 0) {  // no key crosses: both blocks stay as they are
-            if (relayed && (rc = relay_exchange(c, w, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
+            // relay units are 4 bytes on every rank of the stage (coded messages are words)
+            if (relayed && (rc = relay_exchange(c, 4, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
             continue;
         }
         // A sends its top k = A[na-k, na); B sends its bottom k = B[0, k)
@@ -647,11 +712,19 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             sbytes = rbytes = (size_t)k * w;
             nrecv = k;
         }
-        if (relayed) rc = relay_exchange(c, w, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
-        else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
-        if (rc) return rc;
-        c->xchg_bytes += (int64_t)(sbytes + rbytes);
-        if ((rc = do_merge_split(c, dtype, cur, loc, c->recv.p, nrecv, other, keep[st], s))) return rc;
+        const void* rkeys = c->recv.p;
+        if (k > 0 && c->compress) {
+            // delta-code the sorted run; each side sends whichever of coded and raw is
+            // smaller, and the receiver tells them apart by size (coded < raw)
+            if ((rc = coded_exchange(c, dtype, q, relayed, sbuf, k, &rkeys, s))) return rc;
+        } else {
+            if (relayed) rc = relay_exchange(c, 4, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
+            else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
+            if (rc) return rc;
+            c->xchg_bytes += (int64_t)(sbytes + rbytes);
+            c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
+        }
+        if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
         std::swap(cur, other);
     }
     if (cur != out && loc > 0) HIPCHK(hipMemcpyAsync(out, cur, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
@@ -1064,6 +1137,68 @@ int64_t misort_exchange_count(int dtype, const void* samples_min, int64_t n_min,
 int misort_set_relay(misort_ctx* c, int on) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
     c->relay = on != 0;
+    return MISORT_OK;
+}
+
+int misort_codec_probe(misort_ctx* c, int dtype, const void* keys, int64_t n, int reps, float* enc_ms,
+                       float* dec_ms, int64_t* coded_bytes, void* decoded) {
+    if (!c || (dtype != MISORT_U32 && dtype != MISORT_U64) || n <= 0 || !keys || reps < 1)
+        return fail(MISORT_E_INVALID, "bad codec_probe arguments");
+    const size_t w = key_bytes(dtype);
+    int rc;
+    if ((rc = c->enc_send.ensure((size_t)misort::codec_max_words(n, (int)w) * 4))) return rc;
+    const size_t scr = misort::codec_scratch_bytes(n) + 64;
+    if ((rc = c->codec_scr.ensure(scr))) return rc;
+    if ((rc = c->small.ensure(64))) return rc;
+    if ((rc = c->recv.ensure((size_t)n * w))) return rc;
+    void* out = decoded ? decoded : c->recv.p;
+    hipStream_t s = c->stream;
+    hipEvent_t e0, e1, e2;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventCreate(&e2));
+    hipError_t e = hipSuccess;
+    auto enc = [&] {
+        return w == 4 ? misort::codec_encode<uint32_t>((const uint32_t*)keys, n, (uint32_t*)c->enc_send.p,
+                                                      c->codec_scr.p, scr, (uint32_t*)c->small.p, s)
+                      : misort::codec_encode<uint64_t>((const uint64_t*)keys, n, (uint32_t*)c->enc_send.p,
+                                                      c->codec_scr.p, scr, (uint32_t*)c->small.p, s);
+    };
+    auto dec = [&] {
+        return w == 4 ? misort::codec_decode<uint32_t>((const uint32_t*)c->enc_send.p, n, (uint32_t*)out, s)
+                      : misort::codec_decode<uint64_t>((const uint32_t*)c->enc_send.p, n, (uint64_t*)out, s);
+    };
+    e = enc();
+    if (e == hipSuccess) e = hipEventRecord(e0, s);
+    for (int i = 0; i < reps && e == hipSuccess; ++i) e = enc();
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    for (int i = 0; i < reps && e == hipSuccess; ++i) e = dec();
+    if (e == hipSuccess) e = hipEventRecord(e2, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e2);
+    uint32_t words = 0;
+    if (e == hipSuccess) e = hipMemcpy(&words, c->small.p, 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && enc_ms) e = hipEventElapsedTime(enc_ms, e0, e1);
+    if (e == hipSuccess && dec_ms) e = hipEventElapsedTime(dec_ms, e1, e2);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    HIPCHK(e);
+    if (enc_ms) *enc_ms /= reps;
+    if (dec_ms) *dec_ms /= reps;
+    if (coded_bytes) *coded_bytes = (int64_t)words * 4;
+    return MISORT_OK;
+}
+
+int misort_set_compress(misort_ctx* c, int on) {
+    if (!c) return fail(MISORT_E_INVALID, "null ctx");
+    c->compress = on != 0;
+    return MISORT_OK;
+}
+
+int misort_exchange_raw_bytes(misort_ctx* c, int64_t* raw_bytes) {
+    if (!c || !raw_bytes) return fail(MISORT_E_INVALID, "null argument");
+    *raw_bytes = c->xchg_raw_bytes;
+    c->xchg_raw_bytes = 0;
     return MISORT_OK;
 }
 

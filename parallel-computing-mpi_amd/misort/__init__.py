@@ -93,6 +93,10 @@ def lib():
         "misort_comm_init_group": ([vp, vp, i32], i32),
         "misort_set_full_exchange": ([vp, i32], i32),
         "misort_set_relay": ([vp, i32], i32),
+        "misort_set_compress": ([vp, i32], i32),
+        "misort_codec_probe": ([vp, i32, vp, i64, i32, ctypes.POINTER(ctypes.c_float),
+                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i64), vp], i32),
+        "misort_exchange_raw_bytes": ([vp, ctypes.POINTER(i64)], i32),
         "misort_sample_stride": ([i64], i64),
         "misort_sample_count": ([i64], i64),
         "misort_exchange_count": ([i32, vp, i64, vp, i64], i64),
@@ -377,6 +381,24 @@ class Context:
     def set_relay(self, on=True):
         """Spread compare-split exchanges over every xGMI link (P > 2)."""
         _check(lib().misort_set_relay(self._h, int(on)))
+
+    def set_compress(self, on=True):
+        """Delta-code compare-split messages (lossless; default on)."""
+        _check(lib().misort_set_compress(self._h, int(on)))
+
+    def codec_probe(self, keys, decoded=None, reps=3):
+        """Exchange codec on a sorted device run: (encode ms, decode ms, coded bytes)."""
+        a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int64()
+        _check(lib().misort_codec_probe(self._h, _dtype_of(keys), _ptr(keys), keys.numel(), reps,
+                                        ctypes.byref(a), ctypes.byref(b), ctypes.byref(n),
+                                        _ptr(decoded) if decoded is not None else None))
+        return a.value, b.value, int(n.value)
+
+    def exchange_raw_bytes(self):
+        """Bytes the exchanges since the last call would have moved uncoded; resets."""
+        v = ctypes.c_int64()
+        _check(lib().misort_exchange_raw_bytes(self._h, ctypes.byref(v)))
+        return int(v.value)
 
     def exchange_stats(self):
         """(stages, bytes moved, bytes a whole-block exchange would move); resets."""

@@ -56,9 +56,10 @@ def to_host(t, dtype):
     return t.cpu().numpy()
 
 
-def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True):
+def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compress=True, raw=None):
     """Each rank sorts its reference-layout block; returns (concatenated
-    result, check_sort count of every rank, exchange stats of every rank)."""
+    result, check_sort count of every rank, exchange stats of every rank).
+    raw (a dict) receives each rank's uncoded exchange bytes."""
     sizes = misort.block_sizes(x.size, p)
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     max_size = x.size // p + 1
@@ -67,6 +68,7 @@ def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True):
     def rank_fn(r, ctx):
         ctx.set_full_exchange(full_exchange)
         ctx.set_relay(relay)
+        ctx.set_compress(compress)
         buf = to_dev(np.concatenate([blocks[r], np.zeros(max_size - sizes[r], x.dtype)]))
         out = torch.empty_like(buf) if out_of_place else None
         torch.cuda.synchronize()
@@ -75,7 +77,10 @@ def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True):
         errs = ctx.check_sort(res, sizes[r], stream=ctx.native_stream)
         if out_of_place:  # input left unchanged
             np.testing.assert_array_equal(to_host(buf[:sizes[r]], x.dtype), blocks[r])
-        return to_host(res[:sizes[r]], x.dtype), errs, ctx.exchange_stats()
+        st = ctx.exchange_stats()
+        if raw is not None:
+            raw[r] = ctx.exchange_raw_bytes()
+        return to_host(res[:sizes[r]], x.dtype), errs, st
 
     g = misort.Group(p)
     try:
@@ -180,3 +185,46 @@ def test_f64_psort_generator_group_p8_large():
     want = O.parallel_bitonic_sort(x, 8)
     np.testing.assert_array_equal(y.view(np.uint64), want.view(np.uint64))
     assert errs == [O.check_sort(want, 8)] * 8
+
+
+def _u64_mix(n, seed):
+    rng = np.random.default_rng(seed)
+    alpha = rng.integers(0, 2**63, size=1024, dtype=np.uint64)
+    x = np.concatenate([alpha[rng.integers(0, 1024, n // 2)],
+                        np.zeros(n // 8, np.uint64), np.full(n // 8, 2**64 - 1, np.uint64)])
+    x = np.concatenate([x, rng.integers(0, 2**64 - 1, n - x.size, dtype=np.uint64)])
+    rng.shuffle(x)
+    return x
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+@pytest.mark.parametrize("relay", [True, False])
+@pytest.mark.parametrize("kind", ["u32", "u64mix", "f64", "u32dup"])
+def test_coded_exchange_equals_raw(p, relay, kind):
+    """Delta-coded compare-split messages (codec.hip) deliver the same keys as
+    raw ones: u32 uniform (coded ~4x smaller), u64 with 64-bit gaps (0 and
+    all-ones sentinels: width 64, sent raw or coded), the reference's f64
+    generator, and all-duplicate runs (width 0)."""
+    n = (1 << 20) + 7
+    if kind == "u32":
+        x = O.splitmix(0xC0DE + p, n, np.uint32)
+    elif kind == "u32dup":
+        x = (O.splitmix(0xC0DF + p, n, np.uint32) & np.uint32(7)).astype(np.uint32)
+    elif kind == "u64mix":
+        x = _u64_mix(n, p)
+    else:
+        x = O.generate_f64(n)
+    raw_c, raw_r = {}, {}
+    y1, e1, st1 = group_sort(x, p, relay=relay, compress=True, raw=raw_c)
+    y2, e2, st2 = group_sort(x, p, relay=relay, compress=False, raw=raw_r)
+    want = O.parallel_bitonic_sort(x, p)
+    np.testing.assert_array_equal(y1.view(np.uint8), want.view(np.uint8))
+    np.testing.assert_array_equal(y2.view(np.uint8), want.view(np.uint8))
+    assert e1 == e2
+    assert raw_c == raw_r == {r: s[1] for r, s in enumerate(st2)}  # what the raw run moved
+    coded, uncoded = sum(s[1] for s in st1), sum(s[1] for s in st2)
+    assert coded <= uncoded
+    if kind == "u32":  # 2^19 keys per rank: gaps ~2^13, ~16-bit fields
+        assert coded < 0.7 * uncoded
+    if kind == "u32dup":  # gaps 0..7: 3-bit fields
+        assert coded * 5 < uncoded
