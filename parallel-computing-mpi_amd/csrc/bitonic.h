@@ -59,7 +59,7 @@ namespace misort {
 //                          measured table (pass_costs.h); 0: from the model.
 struct PlanKnobs {
     int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
-    int span = 1, row_bytes_log2 = 8, cost_table = 1;
+    int span = 1, row_bytes_log2 = 8, cost_table = 1, wide = 1;
     PlanKnobs();
 };
 const PlanKnobs& plan_knobs();
@@ -837,6 +837,141 @@ void launch_rows(const K* in, K* out, int64_t n, int hi, int R, bool flip, hipSt
     }
 }
 
+// ------------------------------------------------ wide ROWS pass (u32)
+//
+// A ROWS pass over a 2^16-key tile (256 KiB) that lives in registers: 1024
+// lanes x 64 keys, twice the LDS tile.  The tile is 2^R rows at stride 2^lo
+// times 2^(16-R) consecutive keys, so R = 10 strides still read 256-B row runs
+// (the LDS-tile ROWS pass needs 128-B runs for R = 10, which HBM serves ~35 %
+// slower).  Two register layouts, one LDS transpose between them:
+//   load   v = (k << 12) | (t << 2) | q   slot k = the top 4 row bits, whose
+//          stages (flip first: mirrored upper slots, as in k_stream) run in
+//          registers right after the loads; 16 lanes per 256-B row run;
+//   store  v = (t & 63) | (r << 6) | ((t >> 6) << 12)   register r = virtual
+//          bits 6..11, where the other R-4 row stages run; a wave's dword
+//          store covers 64 consecutive keys (one 256-B row run).
+// The transpose moves the tile through the 2^15-key LDS array in two rounds
+// (virtual bit 15 = load slot bit 3 = store lane bit 9), so the pass costs one
+// LDS round trip per key whatever R is (the LDS-tile pass needs two at R >= 9).
+// The DP planner prices it from the measured table like every other shape.
+constexpr int WIDE_LT = 16, WIDE_NT = 1024, WIDE_RMIN = 4, WIDE_RMAX = 10;
+
+// FULL: every key of the tile lies below n (no bounds checks; a separate body
+// so the partial-tile checks do not raise the common path's register use).
+template <int R, bool FLIP, bool FULL>
+__device__ __forceinline__ void rows_wide_tile(const uint32_t* in, uint32_t* out, int64_t n, const TileMap& m,
+                                               int64_t tile, uint32_t* s, int t) {
+    constexpr int LT = WIDE_LT, NT = WIDE_NT, LOADS = 16, V = 4;
+    constexpr bool full = FULL;
+    uint32_t w[LOADS][V];
+    // slot k is row bit group k << (12 - logB): gi(k) = gi(first slot of its half) + (k % 8) << ks
+    const int ks = 12 - (LT - R) + m.lo;
+    const int64_t g0 = tile_index<LT, TM_ROWS>(m, tile, t << 2);
+    const int64_t g8 = FLIP ? tile_index<LT, TM_ROWS>(m, tile, (8 << 12) | ((NT - 1 - t) << 2)) : g0 + ((int64_t)8 << ks);
+#pragma unroll
+    for (int k = 0; k < LOADS; ++k) {
+        const bool mk = FLIP && k >= LOADS / 2;
+        const int64_t gi = (k < 8 ? g0 : g8) + ((int64_t)(k & 7) << ks);
+        uint32_t x[V];
+        if (full) {
+            const KT<uint32_t>::vec y =
+                __builtin_nontemporal_load(reinterpret_cast<const KT<uint32_t>::vec*>(in + gi));
+#pragma unroll
+            for (int j = 0; j < V; ++j) x[j] = y[j];
+        } else {
+            load_vec<uint32_t, false>(in, gi, n, x);
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) w[k][j] = mk ? x[V - 1 - j] : x[j];
+    }
+    // row bits 15..12 (slot bits 3..0), the level's flip first
+    slot_stages<uint32_t, LOADS, 3, 4, FLIP>(w);
+    // transpose, one half of the tile (virtual bit 15 = h) per round
+    uint32_t x[64];
+    const int sb = (t & 63) | (((t >> 6) & 7) << 12);  // store-layout lane bits below bit 15
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();  // round 0's readers are done with the array
+#pragma unroll
+        for (int k = 8 * h; k < 8 * h + 8; ++k) {
+            const bool mk = FLIP && k >= LOADS / 2;
+            const int e = ((k & 7) << 12) | ((mk ? NT - 1 - t : t) << 2);
+#pragma unroll
+            for (int j = 0; j < V; ++j) s[pad(e + j)] = mk ? w[k][V - 1 - j] : w[k][j];
+        }
+        __syncthreads();
+        if ((t >> 9) == h) {
+#pragma unroll
+            for (int r = 0; r < 64; ++r) x[r] = s[pad(sb) + pad(r << 6)];
+        }
+    }
+    // row bits 11..16-R (register bits 5..10-R)
+#pragma unroll
+    for (int r = 5; r > 5 - (R - 4); --r)
+#pragma unroll
+        for (int c = 0; c < 64; ++c)
+            if (!(c & (1 << r))) cx(x[c], x[c | (1 << r)]);
+    // register r: its low CB bits are column bits 6.., the rest row bits
+    constexpr int CB = (LT - R) - 6;
+    const int64_t gs = tile_index<LT, TM_ROWS>(m, tile, (t & 63) | ((t >> 6) << 12));
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+        const int64_t gi = gs + ((r & ((1 << CB) - 1)) << 6) + ((int64_t)(r >> CB) << m.lo);
+        if (full) __builtin_nontemporal_store(x[r], out + gi);
+        else if (gi < n) out[gi] = x[r];
+    }
+}
+
+// Full tiles (every key below n) come first in the tile list; the partial ones
+// (the last 2^(hi+1) segment of a non-power-of-two n) run in a second launch.
+template <int R, bool FLIP, bool FULL>
+__global__ __launch_bounds__(WIDE_NT, 1) void k_rows_wide(const uint32_t* in, uint32_t* out, int64_t n,
+                                                          TileMap m, int64_t tile0) {
+    static_assert(R >= WIDE_RMIN && R <= WIDE_RMAX, "wide ROWS: 4 <= R <= 10");
+    __shared__ uint32_t s[lds_words(1 << (WIDE_LT - 1))];
+    rows_wide_tile<R, FLIP, FULL>(in, out, n, m, tile0 + blockIdx.x, s, threadIdx.x);
+}
+
+template <int R, bool FLIP>
+void launch_wide_rf(const uint32_t* in, uint32_t* out, int64_t n, const TileMap& m, int64_t nfull,
+                    hipStream_t s) {
+    if (nfull > 0) k_rows_wide<R, FLIP, true><<<(unsigned)nfull, WIDE_NT, 0, s>>>(in, out, n, m, 0);
+    if (m.ntiles > nfull)
+        k_rows_wide<R, FLIP, false><<<(unsigned)(m.ntiles - nfull), WIDE_NT, 0, s>>>(in, out, n, m, nfull);
+}
+
+template <int R>
+void launch_wide_r(const uint32_t* in, uint32_t* out, int64_t n, const TileMap& m, int64_t nfull, hipStream_t s) {
+    if (m.flip) launch_wide_rf<R, true>(in, out, n, m, nfull, s);
+    else launch_wide_rf<R, false>(in, out, n, m, nfull, s);
+}
+
+// One wide ROWS pass: strides 2^hi .. 2^(hi-R+1) of a level, 4 <= R <= 10, hi >= 15.
+inline void launch_rows_wide(const uint32_t* in, uint32_t* out, int64_t n, int hi, int R, bool flip,
+                             hipStream_t s) {
+    TileMap m{};
+    m.lo = hi - R + 1;
+    m.hi = hi;
+    m.logB = WIDE_LT - R;
+    m.flip = flip;
+    const int64_t per_seg = ((int64_t)1 << m.lo) >> m.logB;
+    const int64_t full_segs = n >> (hi + 1);
+    const int64_t rem = n - (full_segs << (hi + 1));
+    int64_t part = (rem + ((int64_t)1 << m.logB) - 1) >> m.logB;
+    if (part > per_seg) part = per_seg;
+    m.ntiles = full_segs * per_seg + part;
+    const int64_t nf = full_segs * per_seg;
+    switch (R) {
+        case 4: launch_wide_r<4>(in, out, n, m, nf, s); break;
+        case 5: launch_wide_r<5>(in, out, n, m, nf, s); break;
+        case 6: launch_wide_r<6>(in, out, n, m, nf, s); break;
+        case 7: launch_wide_r<7>(in, out, n, m, nf, s); break;
+        case 8: launch_wide_r<8>(in, out, n, m, nf, s); break;
+        case 9: launch_wide_r<9>(in, out, n, m, nf, s); break;
+        default: launch_wide_r<10>(in, out, n, m, nf, s); break;
+    }
+}
+
 // One HBM pass of the plan.
 struct Pass {
     Kind kind;  // KIND_TILE_SORT, KIND_GLOBAL (ROWS), KIND_SPAN, KIND_TILE_MERGE
@@ -890,30 +1025,38 @@ inline double model_cost(int LT, int KB, int VB, int mode, int R, bool flip, int
 // the model above.  The table captures what the model cannot: rows at some
 // power-of-two strides run up to 40 % slower than at others (HBM channel
 // aliasing), so the planner steers around them.
-inline double pass_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin, int kb, int hi, int k) {
-    const int kind = mode == TM_ROWS ? KIND_GLOBAL : mode == TM_SPAN ? KIND_SPAN : KIND_TILE_MERGE;
-    if (plan_knobs().cost_table) {
-        int best = -1, bd = 1 << 30;
-        for (int i = 0; i < kNumPassCosts; ++i) {
-            const PassCost& e = kPassCosts[i];
-            if (e.key_bytes != kb || e.kind != kind || e.R != R || (e.flip != 0) != flip || e.hi != hi) continue;
-            const int d = e.logn > k ? e.logn - k : k - e.logn;
-            if (d < bd) { bd = d; best = i; }
-        }
-        if (best >= 0) {
-            // unit: the median of the table's passes at that size
-            const int ln = kPassCosts[best].logn;
-            std::vector<float> v;
-            for (int i = 0; i < kNumPassCosts; ++i)
-                if (kPassCosts[i].key_bytes == kb && kPassCosts[i].logn == ln) v.push_back(kPassCosts[i].us);
-            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-            return kPassCosts[best].us / v[v.size() / 2];
-        }
+inline double table_cost(int kind, int kb, int R, bool flip, int hi, int k) {
+    if (!plan_knobs().cost_table) return -1.0;
+    int best = -1, bd = 1 << 30;
+    for (int i = 0; i < kNumPassCosts; ++i) {
+        const PassCost& e = kPassCosts[i];
+        if (e.key_bytes != kb || e.kind != kind || e.R != R || (e.flip != 0) != flip || e.hi != hi) continue;
+        const int d = e.logn > k ? e.logn - k : k - e.logn;
+        if (d < bd) { bd = d; best = i; }
     }
-    return model_cost(LT, KB, VB, mode, R, flip, cmin);
+    if (best < 0) return -1.0;
+    // unit: the median of the table's passes at that size
+    const int ln = kPassCosts[best].logn;
+    std::vector<float> v;
+    for (int i = 0; i < kNumPassCosts; ++i)
+        if (kPassCosts[i].key_bytes == kb && kPassCosts[i].logn == ln) v.push_back(kPassCosts[i].us);
+    std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+    return kPassCosts[best].us / v[v.size() / 2];
 }
 
-inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin, int KB, int VB, int kb) {
+inline double pass_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin, int kb, int hi, int k) {
+    const int kind = mode == TM_ROWS ? KIND_GLOBAL : mode == TM_SPAN ? KIND_SPAN : KIND_TILE_MERGE;
+    const double c = table_cost(kind, kb, R, flip, hi, k);
+    return c >= 0 ? c : model_cost(LT, KB, VB, mode, R, flip, cmin);
+}
+
+// Wide ROWS pass (k_rows_wide): one LDS round trip, rows of 2^(16-R) keys.
+inline double wide_cost(int R, bool flip, int cmin, int hi, int k) {
+    const double c = table_cost(KIND_WIDE, 4, R, flip, hi, k);
+    return c >= 0 ? c : 1.0 + 0.035 + (WIDE_LT - R <= cmin ? 0.03 : 0.0);
+}
+
+inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin, int KB, int VB, int kb, bool wide) {
     struct St { int m, b; };
     std::vector<St> seq;
     for (int m = LT + 1; m <= k; ++m)
@@ -940,6 +1083,11 @@ inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin, int KB, in
                 take(p + R, pass_cost(LT, KB, VB, TM_ROWS, R, b == m - 1, cmin, kb, b, k),
                      Pass{KIND_GLOBAL, b, R, b == m - 1});
             }
+            // the wide (2^16-key register) tile: R <= 10 with >= 2^cmin-key rows
+            for (int R = WIDE_RMIN; wide && R <= WIDE_RMAX && WIDE_LT - R >= cmin && b - R + 1 >= 0; ++R) {
+                if (b - R + 1 < WIDE_LT - R) break;
+                take(p + R, wide_cost(R, b == m - 1, cmin, b, k), Pass{KIND_WIDE, b, R, b == m - 1});
+            }
         } else if (b == LT - 1) {
             take(p + LT, pass_cost(LT, KB, VB, TM_MERGE, 0, false, cmin, kb, LT - 1, k),
                  Pass{KIND_TILE_MERGE, LT - 1, 0, false});
@@ -958,8 +1106,8 @@ inline std::vector<Pass> plan_span(int k, int LT, int rmax, int cmin, int KB, in
     return ps;
 }
 
-inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span, int KB, int VB, int kb) {
-    return span ? plan_span(k, LT, rmax, cmin, KB, VB, kb) : plan_levels(k, LT, rmax);
+inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span, int KB, int VB, int kb, bool wide) {
+    return span ? plan_span(k, LT, rmax, cmin, KB, VB, kb, wide) : plan_levels(k, LT, rmax);
 }
 
 // The plan local_sort_lt runs for n keys (shared with plan_passes()).
@@ -970,7 +1118,9 @@ std::vector<Pass> plan_for(int64_t n) {
     int cmin = kn.row_bytes_log2 - (sizeof(K) == 4 ? 2 : 3);
     if (cmin < 5) cmin = 5;
     typedef TileGeo<K, LT> G;
-    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K));
+    // wide ROWS passes: u32 keys with the 2^15-key LDS tiles (hi >= 15)
+    const bool wide = kn.wide && sizeof(K) == 4 && LTR == WIDE_LT - 1;
+    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K), wide);
 }
 
 // One pass of a plan over n keys, src -> dst.
@@ -989,6 +1139,8 @@ void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hi
         launch_rows<K, LTR, TM_ROWS>(src, dst, n, p.hi, p.R, p.flip, s);
     } else if (p.kind == KIND_SPAN) {
         launch_rows<K, LTR, TM_SPAN>(src, dst, n, p.hi, p.R, true, s);
+    } else if (p.kind == KIND_WIDE) {
+        if constexpr (sizeof(K) == 4) launch_rows_wide(src, dst, n, p.hi, p.R, p.flip, s);
     } else {
         launch_stream<K, LT, TM_MERGE, 0, false, false>(src, dst, n, tm, s);
     }
@@ -1055,6 +1207,11 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_GLOBAL || kind == KIND_SPAN) {
         if (R < 1 || R > S + 1 - 5 || hi - R + 1 < S + 1 - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
+            return hipErrorInvalidValue;
+    }
+    if (kind == KIND_WIDE) {
+        if (sizeof(K) != 4 || R < WIDE_RMIN || R > WIDE_RMAX || hi - R + 1 < WIDE_LT - R ||
+            ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
             return hipErrorInvalidValue;
     }
     if (kn.tile_u32 == 15 && kn.rows_tile_u32 == 15) launch_pass<K, S + 1, S + 1>(in, out, n, p, false, s);

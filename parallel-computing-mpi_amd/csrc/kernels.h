@@ -16,7 +16,8 @@ enum Kind : int {
     KIND_MERGE_SPLIT = 3, // compare-split merge (keep lowest/highest n)
     KIND_OTHER = 4,       // f64 transform, fills, checks
     KIND_SPAN = 5,        // tail of one level + head of the next, row tile
-    KIND_COUNT = 6
+    KIND_WIDE = 6,        // ROWS strides in a 2^16-key register tile (u32)
+    KIND_COUNT = 7
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with

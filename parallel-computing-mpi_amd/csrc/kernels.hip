@@ -21,6 +21,7 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_SPAN", span);
     env("MISORT_COST_TABLE", cost_table);
     env("MISORT_ROW_BYTES_LOG2", row_bytes_log2);
+    env("MISORT_WIDE", wide);
     if (tile_u32 != 14) tile_u32 = 15;
     if (rows_tile_u32 != 14 && tile_u32 == 15) rows_tile_u32 = 15;
     if (tile_u32 != 15) rows_tile_u32 = 14;

@@ -13,6 +13,7 @@ import pytest
 import misort
 
 KIND_SORT, KIND_ROWS, KIND_MERGE, KIND_SPAN = "tile_sort", "global_pass", "tile_merge", "span_pass"
+KIND_WIDE = "wide_pass"  # ROWS stages in the 2^16-key register tile (u32)
 
 
 def ceil_log2(n):
@@ -28,7 +29,7 @@ def plan_stages(plan, lt):
     """Stages the plan's passes run after the SORT pass, as (level, bit)."""
     out = []
     for kind, hi, r, flip in plan[1:]:
-        if kind == KIND_ROWS:
+        if kind in (KIND_ROWS, KIND_WIDE):
             # a ROWS pass runs bits hi..hi-R+1 of the level whose stages they are;
             # the level is known from the flip (hi = m-1) or from the sequence so far
             m = hi + 1 if flip else out[-1][0]
@@ -85,12 +86,15 @@ def test_plan_covers_network(n, key_bytes):
     for kind, hi, r, flip in p[1:]:
         if kind in (KIND_ROWS, KIND_SPAN):
             assert 1 <= r <= lt - 5  # rows keep >= 32 consecutive keys (128 B for u32)
+        if kind == KIND_WIDE:
+            assert key_bytes == 4 and 4 <= r <= 10 and hi >= 15  # >= 64-key rows of a 2^16 tile
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + 29 passes (the level-by-level plan needs 1 + 35)
-    assert len(misort.plan(1 << 30, 4)) == 30
-    assert len(misort.plan(1 << 28, 4)) == 25
+    # 2^30 u32: 1 SORT + 28 passes with wide ROWS passes (1 + 29 without them;
+    # the level-by-level plan needs 1 + 35)
+    assert len(misort.plan(1 << 30, 4)) == 29
+    assert len(misort.plan(1 << 28, 4)) == 24
     assert len(misort.plan(1 << 24, 4)) == 15
     assert any(k == KIND_SPAN for k, *_ in misort.plan(1 << 30, 4))
 
@@ -105,3 +109,44 @@ def test_plan_replay_sorts(n, key_bytes):
     keys[::7] = keys[3]  # duplicates
     got = replay(keys, misort.plan(n, key_bytes), lt)
     np.testing.assert_array_equal(got, np.sort(keys))
+
+
+WIDE_CHILD = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import misort
+print(json.dumps({str(n): misort.plan(n, kb) for n in map(int, sys.argv[2].split(",")) for kb in (4,)}))
+"""
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_plans_with_and_without_wide_passes(wide):
+    """Plans under MISORT_WIDE=0/1 (knobs are read once per process: a child
+    process) cover the network exactly and sort when replayed."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sizes = [(1 << 16) + 3, 100003, (1 << 18) - 5, 1 << 20, 1 << 24, 1 << 28, 1 << 30, 1 << 31]
+    r = subprocess.run([sys.executable, "-c", WIDE_CHILD, os.path.join(root, "parallel-computing-mpi_amd"),
+                        ",".join(map(str, sizes))], env=dict(os.environ, MISORT_WIDE=wide),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plans = {int(k): [tuple(p) for p in v] for k, v in json.loads(r.stdout).items()}
+    lt = misort.tile_log2(4)
+    n_wide = 0
+    for n, p in plans.items():
+        assert plan_stages(p, lt) == network(ceil_log2(n), lt)
+        n_wide += sum(1 for q in p if q[0] == KIND_WIDE)
+        for kind, hi, rr, flip in p:
+            if kind == KIND_WIDE:
+                assert 4 <= rr <= 10 and hi >= 15
+        if n <= 1 << 18:
+            rng = np.random.default_rng(n)
+            keys = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+            np.testing.assert_array_equal(replay(keys, p, lt), np.sort(keys))
+    if wide == "1":
+        assert n_wide > 0 and len(plans[1 << 30]) <= 30
+    else:
+        assert n_wide == 0
