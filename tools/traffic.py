@@ -4,7 +4,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes
 of a 16-B-per-lane streaming read (MI355X_MICROARCH.md, HBM section; confirmed
 on this access shape by profiles/r01/pmc/calfetch_*), so it is doubled.
-Families follow the k_stream TileMode template argument (0 SORT, 1 MERGE, 2 ROWS, 3 SPAN).
+Families follow the k_stream TileMode template argument (0 SORT, 1 MERGE, 2 ROWS, 3 SPAN);
+k_rows_wide (2^16-key register-tile ROWS) is its own family.
     tools/traffic.py gpurun_out/pmc30 > profiles/traffic.json
 """
 import collections
@@ -22,9 +23,13 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
         m = re.search(r"k_stream<unsigned int, (\d+), (\d)", name)
-        if not m:
+        if m:
+            fam = FAMILY[m.group(2)]
+        elif "k_rows_wide" in name:
+            fam = "wide_pass"
+        else:
             continue
-        acc[FAMILY[m.group(2)]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        acc[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {"source": os.path.basename(os.path.normpath(root)),
        "note": "bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE correction)"}
 for fam, cs in acc.items():
