@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "kernels.h"
@@ -1110,9 +1111,26 @@ inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span, int 
     return span ? plan_span(k, LT, rmax, cmin, KB, VB, kb, wide) : plan_levels(k, LT, rmax);
 }
 
-// The plan local_sort_lt runs for n keys (shared with plan_passes()).
+// The plan local_sort_lt runs for n keys (shared with plan_passes()).  It
+// depends only on ceil_log2(n) (the knobs are read once), and the DP over the
+// measured cost table takes milliseconds of host time, so each size is
+// planned once per process: without the cache a 2^20-key sort spent ~0.5 ms
+// per call on the host planning it (profiles/r01/size_sweep_v9.jsonl; 2^24 u32 went 1.47 -> 0.60 ms).
 template <typename K, int LT, int LTR>
-std::vector<Pass> plan_for(int64_t n) {
+std::vector<Pass> plan_uncached(int k);
+
+template <typename K, int LT, int LTR>
+const std::vector<Pass>& plan_for(int64_t n) {
+    static std::mutex mu;
+    static std::vector<Pass> cache[64];
+    const int k = ceil_log2(n);
+    std::lock_guard<std::mutex> g(mu);
+    if (cache[k].empty()) cache[k] = plan_uncached<K, LT, LTR>(k);
+    return cache[k];
+}
+
+template <typename K, int LT, int LTR>
+std::vector<Pass> plan_uncached(int k) {
     const PlanKnobs& kn = plan_knobs();
     const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
     int cmin = kn.row_bytes_log2 - (sizeof(K) == 4 ? 2 : 3);
@@ -1120,7 +1138,7 @@ std::vector<Pass> plan_for(int64_t n) {
     typedef TileGeo<K, LT> G;
     // wide ROWS passes: u32 keys with the 2^15-key LDS tiles (hi >= 15)
     const bool wide = kn.wide && sizeof(K) == 4 && LTR == WIDE_LT - 1;
-    return plan(ceil_log2(n), LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K), wide);
+    return plan(k, LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K), wide);
 }
 
 // One pass of a plan over n keys, src -> dst.
@@ -1151,7 +1169,7 @@ template <typename K, int LT, int LTR>
 hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                          LaunchHook* hook, const StageIO* io) {
     const PlanKnobs& kn = plan_knobs();
-    const std::vector<Pass> ps = plan_for<K, LT, LTR>(n);
+    const std::vector<Pass>& ps = plan_for<K, LT, LTR>(n);
     const int np = (int)ps.size();
     const bool pp = kn.pingpong && scratch != nullptr && scratch != out && scratch != in;
     const double bytes = 2.0 * (double)n * sizeof(K);
