@@ -57,11 +57,23 @@ namespace misort {
 //   MISORT_ROW_BYTES_LOG2  shortest row run a ROWS/SPAN tile may use (default 8:
 //                          256 B; 7 allows 128-B rows);
 //   MISORT_COST_TABLE      1 (default): the planner prices passes from the
-//                          measured table (pass_costs.h); 0: from the model.
+//                          measured table (pass_costs.h); 0: from the model;
+//   MISORT_TILE_LOG2_U64, MISORT_ROWS_TILE_LOG2_U64, MISORT_PERSIST_U64
+//                          the tile sizes (14 or 13) and persistent modes of
+//                          the u64 (and f64) sort, chosen apart from u32's.
+//                          Default 13/13/1: two 512-lane workgroups per CU and
+//                          only the SORT pass persistent -- 8.11 -> 8.76 Gkeys/s
+//                          at 2^29 u64 although the plan has 3 more passes
+//                          (profiles/r01/ab/u64_tiles.txt).
 struct PlanKnobs {
     int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
     int span = 1, row_bytes_log2 = 8, cost_table = 1, wide = 1;
+    int tile_u64 = 13, rows_tile_u64 = 13, persist_u64 = 1;
     PlanKnobs();
+    // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
+    bool big(int kb) const { return kb == 4 ? tile_u32 == 15 : tile_u64 == 14; }
+    bool rbig(int kb) const { return kb == 4 ? rows_tile_u32 == 15 : rows_tile_u64 == 14; }
+    int persist_mask(int kb) const { return kb == 4 ? persist : persist_u64; }
 };
 const PlanKnobs& plan_knobs();
 
@@ -782,7 +794,7 @@ template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD>
 void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
     typedef TileGeo<K, LT> G;
     static int64_t cap = 0;  // resident workgroups for this instantiation
-    const bool persist = (plan_knobs().persist >> MODE) & 1;
+    const bool persist = (plan_knobs().persist_mask((int)sizeof(K)) >> MODE) & 1;
     if (persist && cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;
         (void)hipGetDevice(&dev);
@@ -1013,8 +1025,8 @@ inline std::vector<Pass> plan_levels(int k, int LT, int rmax) {
 // sweep per pass, plus a little per LDS phase of the pass's schedule
 // (prog_plan) and for the shortest (2^cmin-key) rows.  For 2^30 u32 keys this
 // is 1 + 29 passes instead of the level-by-level plan's 1 + 35.
-inline double model_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin) {
-    const bool persist = (plan_knobs().persist >> mode) & 1;
+inline double model_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin, int kb) {
+    const bool persist = (plan_knobs().persist_mask(kb) >> mode) & 1;
     const ProgPlan pp = prog_plan(ProgGeo{LT, KB, VB, mode, R, flip, persist ? 2 : KB});
     const bool short_rows = (mode == TM_ROWS || mode == TM_SPAN) && LT - R <= cmin;
     return 1.0 + 0.035 * pp.phases + (short_rows ? 0.03 : 0.0);
@@ -1026,34 +1038,36 @@ inline double model_cost(int LT, int KB, int VB, int mode, int R, bool flip, int
 // the model above.  The table captures what the model cannot: rows at some
 // power-of-two strides run up to 40 % slower than at others (HBM channel
 // aliasing), so the planner steers around them.
-inline double table_cost(int kind, int kb, int R, bool flip, int hi, int k) {
+inline double table_cost(int kind, int kb, int lt, int R, bool flip, int hi, int k) {
     if (!plan_knobs().cost_table) return -1.0;
     int best = -1, bd = 1 << 30;
     for (int i = 0; i < kNumPassCosts; ++i) {
         const PassCost& e = kPassCosts[i];
-        if (e.key_bytes != kb || e.kind != kind || e.R != R || (e.flip != 0) != flip || e.hi != hi) continue;
+        if (e.key_bytes != kb || e.lt != lt || e.kind != kind || e.R != R || (e.flip != 0) != flip || e.hi != hi)
+            continue;
         const int d = e.logn > k ? e.logn - k : k - e.logn;
         if (d < bd) { bd = d; best = i; }
     }
     if (best < 0) return -1.0;
-    // unit: the median of the table's passes at that size
+    // unit: the median of the table's passes at that size and tile
     const int ln = kPassCosts[best].logn;
     std::vector<float> v;
     for (int i = 0; i < kNumPassCosts; ++i)
-        if (kPassCosts[i].key_bytes == kb && kPassCosts[i].logn == ln) v.push_back(kPassCosts[i].us);
+        if (kPassCosts[i].key_bytes == kb && kPassCosts[i].lt == lt && kPassCosts[i].logn == ln)
+            v.push_back(kPassCosts[i].us);
     std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
     return kPassCosts[best].us / v[v.size() / 2];
 }
 
 inline double pass_cost(int LT, int KB, int VB, int mode, int R, bool flip, int cmin, int kb, int hi, int k) {
     const int kind = mode == TM_ROWS ? KIND_GLOBAL : mode == TM_SPAN ? KIND_SPAN : KIND_TILE_MERGE;
-    const double c = table_cost(kind, kb, R, flip, hi, k);
-    return c >= 0 ? c : model_cost(LT, KB, VB, mode, R, flip, cmin);
+    const double c = table_cost(kind, kb, LT, R, flip, hi, k);
+    return c >= 0 ? c : model_cost(LT, KB, VB, mode, R, flip, cmin, kb);
 }
 
 // Wide ROWS pass (k_rows_wide): one LDS round trip, rows of 2^(16-R) keys.
 inline double wide_cost(int R, bool flip, int cmin, int hi, int k) {
-    const double c = table_cost(KIND_WIDE, 4, R, flip, hi, k);
+    const double c = table_cost(KIND_WIDE, 4, WIDE_LT - 1, R, flip, hi, k);  // measured beside the 2^15 tiles
     return c >= 0 ? c : 1.0 + 0.035 + (WIDE_LT - R <= cmin ? 0.03 : 0.0);
 }
 
@@ -1210,30 +1224,34 @@ hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, h
     if (sizeof(K) == 4 && ord_in) return hipErrorInvalidValue;
     constexpr int S = KT<K>::LT_SMALL;  // 14 (u32) / 13 (u64): the 64 KiB tile
     const PlanKnobs& kn = plan_knobs();
-    const bool big = kn.tile_u32 == 15, rbig = kn.rows_tile_u32 == 15;
+    const bool big = kn.big((int)sizeof(K)), rbig = kn.rbig((int)sizeof(K));
     if (big && rbig) return local_sort_lt<K, S + 1, S + 1>(in, out, n, ord_in, scratch, s, hook, io);
     if (big) return local_sort_lt<K, S + 1, S>(in, out, n, ord_in, scratch, s, hook, io);
     return local_sort_lt<K, S, S>(in, out, n, ord_in, scratch, s, hook, io);
 }
 
-// One pass of any shape (pass-cost probes, tools/pass_costs.py).
+// One pass of any shape (pass-cost probes, tools/pass_costs.py), with the key
+// type's current tiles (both large or both small).
 template <typename K>
 hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int flip, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     constexpr int S = KT<K>::LT_SMALL;
     const PlanKnobs& kn = plan_knobs();
+    const bool big = kn.big((int)sizeof(K)), rbig = kn.rbig((int)sizeof(K));
+    if (big != rbig) return hipErrorInvalidValue;
+    const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_GLOBAL || kind == KIND_SPAN) {
-        if (R < 1 || R > S + 1 - 5 || hi - R + 1 < S + 1 - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
+        if (R < 1 || R > LT - 5 || hi - R + 1 < LT - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
             return hipErrorInvalidValue;
     }
     if (kind == KIND_WIDE) {
-        if (sizeof(K) != 4 || R < WIDE_RMIN || R > WIDE_RMAX || hi - R + 1 < WIDE_LT - R ||
+        if (sizeof(K) != 4 || !big || R < WIDE_RMIN || R > WIDE_RMAX || hi - R + 1 < WIDE_LT - R ||
             ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
             return hipErrorInvalidValue;
     }
-    if (kn.tile_u32 == 15 && kn.rows_tile_u32 == 15) launch_pass<K, S + 1, S + 1>(in, out, n, p, false, s);
-    else return hipErrorInvalidValue;
+    if (big) launch_pass<K, S + 1, S + 1>(in, out, n, p, false, s);
+    else launch_pass<K, S, S>(in, out, n, p, false, s);
     return hipGetLastError();
 }
 

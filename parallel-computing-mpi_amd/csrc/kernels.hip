@@ -22,6 +22,12 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_COST_TABLE", cost_table);
     env("MISORT_ROW_BYTES_LOG2", row_bytes_log2);
     env("MISORT_WIDE", wide);
+    env("MISORT_TILE_LOG2_U64", tile_u64);
+    env("MISORT_ROWS_TILE_LOG2_U64", rows_tile_u64);
+    env("MISORT_PERSIST_U64", persist_u64);
+    if (tile_u64 != 13) tile_u64 = 14;
+    if (rows_tile_u64 != 13 && tile_u64 == 14) rows_tile_u64 = 14;
+    if (tile_u64 != 14) rows_tile_u64 = 13;
     if (tile_u32 != 14) tile_u32 = 15;
     if (rows_tile_u32 != 14 && tile_u32 == 15) rows_tile_u32 = 15;
     if (tile_u32 != 15) rows_tile_u32 = 14;
@@ -36,15 +42,15 @@ const PlanKnobs& plan_knobs() {
 
 // Tile size per key type (log2 keys of the SORT/MERGE tile).
 int tile_log2(int key_bytes) {
-    const int u32 = plan_knobs().tile_u32;
-    return key_bytes == 4 ? u32 : u32 - 1;
+    const PlanKnobs& kn = plan_knobs();
+    return key_bytes == 4 ? kn.tile_u32 : kn.tile_u64;
 }
 
 int plan_passes(int64_t n, int key_bytes, int* out, int max) {
     if (n <= 0) return 0;
     constexpr int S = KT<uint32_t>::LT_SMALL;
     const PlanKnobs& kn = plan_knobs();
-    const bool big = kn.tile_u32 == 15, rbig = kn.rows_tile_u32 == 15;
+    const bool big = kn.big(key_bytes), rbig = kn.rbig(key_bytes);
     std::vector<Pass> ps;
     if (key_bytes == 4) {
         ps = big && rbig ? plan_for<uint32_t, S + 1, S + 1>(n)
