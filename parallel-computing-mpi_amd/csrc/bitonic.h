@@ -64,11 +64,12 @@ namespace misort {
 //                          Default 13/13/1: two 512-lane workgroups per CU and
 //                          only the SORT pass persistent -- 8.11 -> 8.76 Gkeys/s
 //                          at 2^29 u64 although the plan has 3 more passes
-//                          (profiles/r01/ab/u64_tiles.txt).
+//                          (profiles/r01/ab/u64_tiles.txt);
+//   MISORT_SORT_U32        1 (default): the u32 SORT pass runs k_sort_u32; 0: k_stream.
 struct PlanKnobs {
     int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
     int span = 1, row_bytes_log2 = 8, cost_table = 1, wide = 1;
-    int tile_u64 = 13, rows_tile_u64 = 13, persist_u64 = 1;
+    int tile_u64 = 13, rows_tile_u64 = 13, persist_u64 = 1, sort_u32 = 1;
     PlanKnobs();
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
     bool big(int kb) const { return kb == 4 ? tile_u32 == 15 : tile_u64 == 14; }
@@ -850,6 +851,112 @@ void launch_rows(const K* in, K* out, int64_t n, int hi, int R, bool flip, hipSt
     }
 }
 
+// ------------------------------------------------ u32 SORT pass kernel
+//
+// k_stream<SORT>'s body for u32 keys (in-wave levels 1..MISORT_WAVE_LEVELS,
+// LDS phases above), with the full/partial tile split made at compile time:
+// the persistent grid walks only full tiles, and a one-workgroup launch sorts
+// the partial last tile.  Inside k_stream the bounds-checked load/store paths
+// pushed the persistent SORT kernel to 128 VGPRs with spills, and one spill
+// reload right after the next tile's prefetch issued an s_waitcnt vmcnt(0)
+// that waited for the whole prefetch (vmcnt is in order), so the prefetch hid
+// nothing.  The tile base is uniform (SGPRs); lanes add 32-bit offsets.
+template <bool FULL>
+__device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* in, int64_t tile, int64_t n, int t) {
+    const uint32_t* tb = in + (tile << 15);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int e = place<uint32_t, 15, 12>(k, t);
+        if constexpr (FULL) {
+            const KT<uint32_t>::vec x = __builtin_nontemporal_load(reinterpret_cast<const KT<uint32_t>::vec*>(tb + e));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pre[k][j] = x[j];
+        } else {
+            load_vec<uint32_t, false>(in, (tile << 15) + e, n, pre[k]);
+        }
+    }
+}
+
+template <bool PERSIST, bool FULL>
+__global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, TileMap m,
+                                                      int64_t tile0) {
+    typedef uint32_t K;
+    constexpr int LT = 15;
+    typedef TileGeo<K, LT> G;
+    constexpr ProgPlan P = prog_plan(ProgGeo{LT, G::KB, G::VB, TM_SORT, 0, false, PERSIST ? 2 : G::KB});
+    constexpr int SL = LT - G::KB, WL = MISORT_WAVE_LEVELS;
+    static_assert(G::LOADS == 8 && G::NT == 1024 && WL >= 5 && WL <= 10, "u32 SORT tile shape");
+    __shared__ K s[lds_words(G::T)];
+    int64_t tile = tile0 + blockIdx.x;
+    if (tile >= m.ntiles) return;
+    K pre[G::LOADS][G::V];
+    sort_fetch<FULL>(pre, in, tile, n, (int)threadIdx.x);
+    for (; tile < m.ntiles; tile += gridDim.x) {
+        // lane id through an opaque copy: the per-lane LDS/HBM addresses are
+        // recomputed every tile instead of being hoisted into ~16 loop-invariant
+        // VGPRs (which pushed the kernel into spills)
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        const int a0 = pad(t << 5);
+        slot_stages<K, G::LOADS, P.PRE_TOP, P.PRE, P.PRE_FLIP>(pre);
+#pragma unroll
+        for (int k = 0; k < G::LOADS; ++k) {
+            const int e = place<K, LT, SL>(k, t);
+#pragma unroll
+            for (int j = 0; j < G::V; ++j) s[pad(e + j)] = pre[k][j];
+        }
+        __syncthreads();
+        uint32_t x[32];
+#pragma unroll
+        for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
+        reg_stages_c<uint32_t, 0, 1, true>(x);
+        reg_stages_c<uint32_t, 1, 2, true>(x);
+        reg_stages_c<uint32_t, 2, 3, true>(x);
+        reg_stages_c<uint32_t, 3, 4, true>(x);
+        reg_stages_c<uint32_t, 4, 5, true>(x);
+        wave_levels<6, WL>(x, t & 63);
+        // each lane rewrites only the keys it read: no barrier before
+#pragma unroll
+        for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
+        __syncthreads();
+        // the next tile's loads fly during the LDS phases (issued here, not
+        // before the wave levels, so their registers and the cross-lane
+        // temporaries are never live together)
+        const int64_t nxt = tile + gridDim.x;
+        if (PERSIST && nxt < m.ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
+        sort_levels<K, WL + 1, LT>(s, t);
+        final_store<K, LT, TM_SORT, SL, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n, FULL,
+                                                                                         t);
+        if constexpr (!PERSIST) break;
+        __syncthreads();
+    }
+}
+
+inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+    static int64_t cap = 0;
+    TileMap m{};
+    const int64_t nfull = n >> 15;
+    const bool persist = plan_knobs().persist & 1;
+    if (persist && cap == 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<true, true>, 1024, 0);
+        cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
+    }
+    if (nfull > 0) {
+        m.ntiles = nfull;
+        const int64_t want = persist ? cap * plan_knobs().grid_mult : nfull;
+        const int64_t grid = nfull < want ? nfull : want;
+        if (persist) k_sort_u32<true, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0);
+        else k_sort_u32<false, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0);
+    }
+    if ((nfull << 15) < n) {
+        m.ntiles = nfull + 1;
+        k_sort_u32<false, false><<<1, 1024, 0, s>>>(in, out, n, m, nfull);
+    }
+}
+
 // ------------------------------------------------ wide ROWS pass (u32)
 //
 // A ROWS pass over a 2^16-key tile (256 KiB) that lives in registers: 1024
@@ -928,7 +1035,7 @@ __device__ __forceinline__ void rows_wide_tile(const uint32_t* in, uint32_t* out
     constexpr int CB = (LT - R) - 6;
     const int64_t gs = tile_index<LT, TM_ROWS>(m, tile, (t & 63) | ((t >> 6) << 12));
 #pragma unroll
-    for (int r = 0; r < 64; ++r) {
+    for (int r = 63; r >= 0; --r) {
         const int64_t gi = gs + ((r & ((1 << CB) - 1)) << 6) + ((int64_t)(r >> CB) << m.lo);
         if (full) __builtin_nontemporal_store(x[r], out + gi);
         else if (gi < n) out[gi] = x[r];
@@ -1164,6 +1271,8 @@ void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hi
         if constexpr (sizeof(K) == 8) {
             if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
             else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+        } else if (LT == 15 && MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 10 && plan_knobs().sort_u32) {
+            launch_sort_u32(src, dst, n, s);
         } else {
             launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
         }

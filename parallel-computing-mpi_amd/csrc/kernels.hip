@@ -25,6 +25,7 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_TILE_LOG2_U64", tile_u64);
     env("MISORT_ROWS_TILE_LOG2_U64", rows_tile_u64);
     env("MISORT_PERSIST_U64", persist_u64);
+    env("MISORT_SORT_U32", sort_u32);
     if (tile_u64 != 13) tile_u64 = 14;
     if (rows_tile_u64 != 13 && tile_u64 == 14) rows_tile_u64 = 14;
     if (tile_u64 != 14) rows_tile_u64 = 13;
