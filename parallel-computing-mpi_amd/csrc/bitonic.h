@@ -344,6 +344,44 @@ __device__ __forceinline__ void sort_levels(K* s, int t) {
     }
 }
 
+// ------------------------------------------------ wave-local LDS phases
+//
+// With 32 consecutive keys per lane, a wave owns the 2^11 keys v>>11 == wave.
+// An LDS phase whose window lies below bit 11 (B <= 6) touches only its wave's
+// keys, so between two such phases the wave needs no workgroup barrier: LDS
+// ops of one wave execute in order, and a compiler barrier keeps the reads
+// after the writes.  Levels 9..11 then run without s_barrier and the waves
+// drift apart, overlapping one wave's LDS traffic with another's min/max; a
+// barrier remains around every phase whose window reaches bit 11.
+constexpr int WAVE_BITS = 11;
+#ifndef MISORT_SORT_WAVE_SYNC
+#define MISORT_SORT_WAVE_SYNC 1
+#endif
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
+
+// Strides HI..STOP (flip first); NEXT_HI: top bit of the phase after the range
+// (-1: what follows reads across waves).
+template <typename K, int HI, int STOP, bool FLIP, int NEXT_HI>
+__device__ __forceinline__ void lds_range_w(K* s, int t) {
+    if constexpr (HI >= STOP) {
+        constexpr int B = HI > 4 ? HI - 4 : 0;
+        constexpr int LOWEST = B > STOP ? B : STOP;
+        phase_c<K, B, HI - B, HI - LOWEST + 1, FLIP>(s, t);
+        constexpr int NXT = LOWEST - 1 >= STOP ? LOWEST - 1 : NEXT_HI;
+        if constexpr (!MISORT_SORT_WAVE_SYNC || HI >= WAVE_BITS || NXT >= WAVE_BITS || NXT < 0) __syncthreads();
+        else wave_sync();
+        lds_range_w<K, LOWEST - 1, STOP, false, NEXT_HI>(s, t);
+    }
+}
+
+template <typename K, int L, int LT>
+__device__ __forceinline__ void sort_levels_w(K* s, int t) {
+    if constexpr (L <= LT) {
+        lds_range_w<K, L - 1, 0, true, (L < LT ? L : -1)>(s, t);
+        sort_levels_w<K, L + 1, LT>(s, t);
+    }
+}
+
 // ------------------------------------------------ in-wave tile sort (u32)
 //
 // The SORT pass for u32 keys keeps each wave's 2^11 keys in registers for
@@ -755,11 +793,12 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
 #pragma unroll
                     for (int c = 0; c < 32; ++c) s[a0 + c] = v[c];
                 }
-                __syncthreads();
-                sort_levels<K, 6, LT>(s, t);
+                if constexpr (MISORT_SORT_WAVE_SYNC) wave_sync();  // level 6 stays inside the wave
+                else __syncthreads();
+                sort_levels_w<K, 6, LT>(s, t);
             } else {
-                lds_range<K, P.T_HI, P.T_LO, false>(s, t);
-                lds_range<K, P.H_HI, P.H_LO, true>(s, t);
+                lds_range_w<K, P.T_HI, P.T_LO, false, (P.H_HI >= P.H_LO ? P.H_HI : -1)>(s, t);
+                lds_range_w<K, P.H_HI, P.H_LO, true, -1>(s, t);
             }
             // LDS -> registers (final slot window) -> last stages -> HBM
             constexpr int SF = MODE == TM_SORT ? LT - G::KB : P.SF;
@@ -915,16 +954,18 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
         reg_stages_c<uint32_t, 3, 4, true>(x);
         reg_stages_c<uint32_t, 4, 5, true>(x);
         wave_levels<6, WL>(x, t & 63);
-        // each lane rewrites only the keys it read: no barrier before
+        // each lane rewrites only the keys it read: no barrier before, and the
+        // next phase (level WL+1 <= 11) stays inside the wave
 #pragma unroll
         for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
-        __syncthreads();
+        if constexpr (WL + 1 <= WAVE_BITS && MISORT_SORT_WAVE_SYNC) wave_sync();
+        else __syncthreads();
         // the next tile's loads fly during the LDS phases (issued here, not
         // before the wave levels, so their registers and the cross-lane
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < m.ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
-        sort_levels<K, WL + 1, LT>(s, t);
+        sort_levels_w<K, WL + 1, LT>(s, t);
         final_store<K, LT, TM_SORT, SL, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n, FULL,
                                                                                          t);
         if constexpr (!PERSIST) break;
