@@ -53,7 +53,9 @@ enum misort_kernel_kind {
     MISORT_K_TILE_MERGE = 2,  /* in-tile strides of one merge level      */
     MISORT_K_MERGE_SPLIT = 3, /* device compare-split (psort.cc:116-164) */
     MISORT_K_OTHER = 4,
-    MISORT_K_SPAN = 5         /* tail of one level + head of the next    */
+    MISORT_K_SPAN = 5,        /* tail of one level + head of the next    */
+    MISORT_K_WIDE = 6,        /* ROWS strides in a 2^16-key register tile */
+    MISORT_K_RUN_MERGE = 7    /* one merge level: runs 2^hi -> 2^(hi+1)  */
 };
 
 typedef struct misort_ctx misort_ctx;

@@ -70,7 +70,12 @@ struct PlanKnobs {
     int tile_u32 = 15, rows_tile_u32 = 15, rmax = 10, persist = 3 | 8, grid_mult = 1, pingpong = 1;
     int span = 1, row_bytes_log2 = 8, cost_table = 1, wide = 1;
     int tile_u64 = 13, rows_tile_u64 = 13, persist_u64 = 1, sort_u32 = 1;
+    // first level finished by merge passes (runs.hip) instead of the network
+    // (0 = network only), per key type.  Measured at 2^30 u32 / 2^29 u64: the
+    // SORT tile's level is best (profiles/r01/runs/).
+    int merge_from_u32 = 15, merge_from_u64 = 13;
     PlanKnobs();
+    int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
     bool big(int kb) const { return kb == 4 ? tile_u32 == 15 : tile_u64 == 14; }
     bool rbig(int kb) const { return kb == 4 ? rows_tile_u32 == 15 : rows_tile_u64 == 14; }
@@ -1278,22 +1283,32 @@ inline std::vector<Pass> plan(int k, int LT, int rmax, int cmin, bool span, int 
 // measured cost table takes milliseconds of host time, so each size is
 // planned once per process: without the cache a 2^20-key sort spent ~0.5 ms
 // per call on the host planning it (profiles/r01/size_sweep_v9.jsonl; 2^24 u32 went 1.47 -> 0.60 ms).
+//
+// runs: the sort has a scratch buffer to ping-pong with, so levels from
+// merge_from on may run as merge passes (KIND_RUNS, hi = log2 of the input
+// run length), one HBM pass per level instead of about two network passes.
 template <typename K, int LT, int LTR>
-std::vector<Pass> plan_uncached(int k);
+std::vector<Pass> plan_uncached(int k, bool runs);
 
 template <typename K, int LT, int LTR>
-const std::vector<Pass>& plan_for(int64_t n) {
+const std::vector<Pass>& plan_for(int64_t n, bool runs = true) {
     static std::mutex mu;
-    static std::vector<Pass> cache[64];
+    static std::vector<Pass> cache[2][64];
     const int k = ceil_log2(n);
     std::lock_guard<std::mutex> g(mu);
-    if (cache[k].empty()) cache[k] = plan_uncached<K, LT, LTR>(k);
-    return cache[k];
+    if (cache[runs][k].empty()) cache[runs][k] = plan_uncached<K, LT, LTR>(k, runs);
+    return cache[runs][k];
 }
 
 template <typename K, int LT, int LTR>
-std::vector<Pass> plan_uncached(int k) {
+std::vector<Pass> plan_uncached(int k, bool runs) {
     const PlanKnobs& kn = plan_knobs();
+    const int m0 = kn.merge_from((int)sizeof(K));
+    if (runs && m0 > 0 && k > m0) {
+        std::vector<Pass> ps = plan_uncached<K, LT, LTR>(m0 < LT ? LT : m0, false);
+        for (int lw = m0 < LT ? LT : m0; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
+        return ps;
+    }
     const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
     int cmin = kn.row_bytes_log2 - (sizeof(K) == 4 ? 2 : 3);
     if (cmin < 5) cmin = 5;
@@ -1333,9 +1348,9 @@ template <typename K, int LT, int LTR>
 hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                          LaunchHook* hook, const StageIO* io) {
     const PlanKnobs& kn = plan_knobs();
-    const std::vector<Pass>& ps = plan_for<K, LT, LTR>(n);
-    const int np = (int)ps.size();
     const bool pp = kn.pingpong && scratch != nullptr && scratch != out && scratch != in;
+    const std::vector<Pass>& ps = plan_for<K, LT, LTR>(n, pp);  // merge passes need two buffers
+    const int np = (int)ps.size();
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
     for (int i = 0; i < np; ++i) {
@@ -1343,7 +1358,8 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
-        const bool contig = p.kind == KIND_TILE_SORT || p.kind == KIND_TILE_MERGE;
+        const bool runs = p.kind == KIND_RUNS;
+        const bool contig = p.kind == KIND_TILE_SORT || p.kind == KIND_TILE_MERGE || runs;
         const bool cin = io && io->before_first && i == 0;
         const bool cout = io && io->after_last && i == np - 1 && contig;
         if (cin || cout) {
@@ -1353,9 +1369,17 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
             for (int64_t k0 = 0; k0 < n; k0 += ch) {
                 const int64_t k1 = n - k0 < ch ? n : k0 + ch;
                 if (cin && io->before_first(k0, k1, s)) return hipErrorUnknown;
-                launch_pass<K, LT, LTR>(src + k0, dst + k0, k1 - k0, p, ord_in, s);
+                if (runs) {
+                    // a merge level reads across chunks: whole input, output range [k0, k1)
+                    if (merge_level<K>(src, dst, n, p.hi, s, k0, k1) != hipSuccess) return hipErrorInvalidValue;
+                } else {
+                    launch_pass<K, LT, LTR>(src + k0, dst + k0, k1 - k0, p, ord_in, s);
+                }
                 if (cout && io->after_last(k0, k1, s)) return hipErrorUnknown;
             }
+        } else if (runs) {
+            const hipError_t e = merge_level<K>(src, dst, n, p.hi, s);
+            if (e != hipSuccess) return e;
         } else {
             launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s);
         }
@@ -1391,6 +1415,8 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     if (big != rbig) return hipErrorInvalidValue;
     const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
+    if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);  // runs of 2^hi -> 2^(hi+1)
+    if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER) return hipErrorInvalidValue;
     if (kind == KIND_GLOBAL || kind == KIND_SPAN) {
         if (R < 1 || R > LT - 5 || hi - R + 1 < LT - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
             return hipErrorInvalidValue;

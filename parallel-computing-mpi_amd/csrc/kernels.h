@@ -17,7 +17,8 @@ enum Kind : int {
     KIND_OTHER = 4,       // f64 transform, fills, checks
     KIND_SPAN = 5,        // tail of one level + head of the next, row tile
     KIND_WIDE = 6,        // ROWS strides in a 2^16-key register tile (u32)
-    KIND_COUNT = 7
+    KIND_RUNS = 7,        // one merge level: runs of 2^hi keys -> runs of 2^(hi+1)
+    KIND_COUNT = 8
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with
@@ -71,6 +72,13 @@ hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
 template <typename K>
 hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, int64_t* scratch, hipStream_t s,
                       LaunchHook* hook);
+
+// One merge level of the local sort (runs.hip): src holds ascending runs of
+// 2^lw keys (the last may be short), dst gets the ascending runs of 2^(lw+1).
+// Only output keys [o0, o1) are written (o0 a multiple of 4096, o1 of 4096 or
+// n; o1 <= 0 means n): the chunked last pass of host staging.  src != dst.
+template <typename K>
+hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0);
 
 // psort.cc:88-101 lower_bound on a sorted device run: *d_out = first i with
 // x <= a[i], or n.

@@ -26,6 +26,8 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_ROWS_TILE_LOG2_U64", rows_tile_u64);
     env("MISORT_PERSIST_U64", persist_u64);
     env("MISORT_SORT_U32", sort_u32);
+    env("MISORT_MERGE_FROM", merge_from_u32);
+    env("MISORT_MERGE_FROM_U64", merge_from_u64);
     if (tile_u64 != 13) tile_u64 = 14;
     if (rows_tile_u64 != 13 && tile_u64 == 14) rows_tile_u64 = 14;
     if (tile_u64 != 14) rows_tile_u64 = 13;

@@ -1,0 +1,232 @@
+// runs.hip -- merge levels of the local sort (gfx950): ascending runs of 2^lw
+// keys -> ascending runs of 2^(lw+1), one HBM read + one HBM write per key.
+//
+// The reference's local sort is std::sort (psort.cc:175); the bitonic network of
+// bitonic.h replaces it up to some level, and from there each remaining level
+// of the sort is a pairwise merge of neighbouring runs.  A bitonic level costs
+// about two HBM passes once its strides leave the LDS tile (2^30 u32: 28 passes
+// for levels 16..30); a merge level costs one.  Output is bit-identical: the
+// keys carry no payload, so every correct sort of them writes the same bytes.
+//
+// Per level, two launches:
+//   k_runs_partition  one lane per output tile: the merge-path co-rank of the
+//                     tile's first output within its pair (binary search, A
+//                     first on ties);
+//   k_runs_merge      one workgroup per output tile of NT*IT keys: its A and B
+//                     ranges are streamed into LDS, each lane finds its own
+//                     co-rank in LDS and merges IT consecutive outputs, and the
+//                     tile leaves through LDS as 16-byte non-temporal stores.
+#include "kernels.h"
+
+#include <map>
+#include <mutex>
+
+namespace misort {
+namespace {
+
+template <typename K>
+struct RunKT;
+template <>
+struct RunKT<uint32_t> {
+    static constexpr int IT = 16;  // 4096-key tiles, 16 KiB of LDS (IT 32: 1.56x slower)
+    static constexpr int V = 4;
+    typedef uint32_t vec __attribute__((ext_vector_type(4)));
+};
+template <>
+struct RunKT<uint64_t> {
+    static constexpr int IT = 16;  // 4096-key tiles, 32 KiB of LDS (IT 8: -2 %)
+    static constexpr int V = 2;
+    typedef uint64_t vec __attribute__((ext_vector_type(2)));
+};
+
+constexpr int RUN_NT = 256;
+
+template <typename K>
+constexpr K KT_MAX = (K)~(K)0;
+
+struct PairGeo {
+    int64_t base, na, nb;
+};
+
+__device__ __forceinline__ PairGeo pair_geo(int64_t g, int64_t n, int lw) {
+    const int64_t w = (int64_t)1 << lw;
+    const int64_t base = (g >> (lw + 1)) << (lw + 1);
+    const int64_t rest = n - base;
+    const int64_t na = rest < w ? rest : w;
+    const int64_t rb = rest - w;
+    const int64_t nb = rb <= 0 ? 0 : (rb < w ? rb : w);
+    return PairGeo{base, na, nb};
+}
+
+// Number of A keys among the first d outputs of merge(A, B), A first on ties.
+template <typename K>
+__device__ int64_t run_corank(const K* __restrict__ A, int64_t na, const K* __restrict__ B, int64_t nb,
+                              int64_t d) {
+    int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (A[mid] <= B[d - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <typename K, int IT>
+__global__ void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, int64_t t0, int64_t ntiles,
+                                 int64_t* __restrict__ co) {
+    constexpr int TILE = RUN_NT * IT;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntiles) return;
+    const int64_t g0 = (t0 + i) * TILE;
+    const PairGeo p = pair_geo(g0, n, lw);
+    const K* A = src + p.base;
+    co[i] = run_corank(A, p.na, A + ((int64_t)1 << lw), p.nb, g0 - p.base);
+}
+
+template <typename K, int IT>
+__global__ __launch_bounds__(RUN_NT) void k_runs_merge(const K* __restrict__ src, K* __restrict__ dst,
+                                                       int64_t n, int lw, int64_t t0,
+                                                       const int64_t* __restrict__ co) {
+    constexpr int V = RunKT<K>::V, TILE = RUN_NT * IT;
+    typedef typename RunKT<K>::vec vec;
+    __shared__ __attribute__((aligned(16))) K s[TILE];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    const int64_t g0 = (t0 + t) * TILE;
+    const int64_t g1 = g0 + TILE < n ? g0 + TILE : n;
+    const PairGeo p = pair_geo(g0, n, lw);
+    const int64_t i0 = co[t];
+    const int64_t i1 = g1 == p.base + p.na + p.nb ? p.na : co[t + 1];
+    const int64_t j0 = g0 - p.base - i0, j1 = g1 - p.base - i1;
+    const int la = (int)(i1 - i0), lb = (int)(j1 - j0), len = la + lb;
+    const K* __restrict__ A = src + p.base + i0;
+    const K* __restrict__ B = src + p.base + ((int64_t)1 << lw) + j0;
+    // s = A range ++ B range: all IT loads of a lane are issued before the
+    // first LDS write (one memory latency per tile, not one per key)
+    {
+        K x[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int e = k * RUN_NT + tid;
+            const K* q = e < la ? A + e : B + (e - la);
+            x[k] = e < len ? __builtin_nontemporal_load(q) : KT_MAX<K>;
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k) s[k * RUN_NT + tid] = x[k];
+    }
+    __syncthreads();
+
+    // this lane's outputs [dk, dk + IT) of the tile
+    const int dk = tid * IT < len ? tid * IT : len;
+    int lo = dk - lb > 0 ? dk - lb : 0, hi = dk < la ? dk : la;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s[mid] <= s[la + dk - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int ia = lo, ib = dk - lo;
+    K av = s[ia < la ? ia : 0], bv = s[ib < lb ? la + ib : 0];
+    K r[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const bool takeA = ia < la && (ib >= lb || av <= bv);
+        r[k] = takeA ? av : bv;
+        ia += takeA;
+        ib += !takeA;
+        const int nx = takeA ? (ia < la ? ia : 0) : (ib < lb ? la + ib : 0);
+        const K v = s[nx];
+        av = takeA ? v : av;
+        bv = takeA ? bv : v;
+    }
+    __syncthreads();
+    if (dk + IT <= len) {
+#pragma unroll
+        for (int k = 0; k < IT; k += V) {
+            vec x;
+#pragma unroll
+            for (int e = 0; e < V; ++e) x[e] = r[k + e];
+            *reinterpret_cast<vec*>(s + dk + k) = x;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (dk + k < len) s[dk + k] = r[k];
+    }
+    __syncthreads();
+    K* __restrict__ out = dst + g0;
+    if (len == TILE) {
+#pragma unroll
+        for (int k = 0; k < IT / V; ++k) {
+            const int e = (k * RUN_NT + tid) * V;
+            __builtin_nontemporal_store(*reinterpret_cast<const vec*>(s + e), reinterpret_cast<vec*>(out + e));
+        }
+    } else {
+        for (int k = tid; k < len; k += RUN_NT) out[k] = s[k];
+    }
+}
+
+// Co-rank scratch: one grow-only buffer per (device, stream), so sorts on
+// different streams (the in-process group drives several ranks from one
+// process, possibly on one device) never share it; on one stream the launches
+// are ordered.
+std::mutex g_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_scratch;
+
+int64_t* corank_scratch(size_t bytes, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto& e = g_scratch[{dev, s}];
+    if (e.second < bytes) {
+        // the old buffer may still be read by launches queued on s
+        if (e.first && (hipStreamSynchronize(s) != hipSuccess || hipFree(e.first) != hipSuccess)) return nullptr;
+        e = {nullptr, 0};
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        e = {p, bytes};
+    }
+    return (int64_t*)e.first;
+}
+
+template <typename K, int IT>
+hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
+    constexpr int TILE = RUN_NT * IT;
+    if (o1 <= 0 || o1 > n) o1 = n;
+    if (n <= 0 || o0 >= o1) return hipSuccess;
+    if (lw < 12 || lw > 40 || ((int64_t)1 << lw) < TILE || src == dst || o0 < 0 || o0 % TILE ||
+        (o1 != n && o1 % TILE))
+        return hipErrorInvalidValue;
+    const int64_t t0 = o0 / TILE, ntiles = (o1 - o0 + TILE - 1) / TILE;
+    // co[i] for tiles t0 .. t0 + ntiles (the one past the range bounds the last)
+    const int64_t nco = t0 + ntiles < (n + TILE - 1) / TILE ? ntiles + 1 : ntiles;
+    int64_t* co = corank_scratch((size_t)(ntiles + 1) * sizeof(int64_t), s);
+    if (!co) return hipErrorOutOfMemory;
+    k_runs_partition<K, IT><<<(unsigned)((nco + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
+    k_runs_merge<K, IT><<<(unsigned)ntiles, RUN_NT, 0, s>>>(src, dst, n, lw, t0, co);
+    return hipGetLastError();
+}
+
+// MISORT_RUN_IT: keys per lane of the merge tile (u32 16 or 32, u64 16 or 32).
+int run_it_knob() {
+    static const int v = [] {
+        const char* e = getenv("MISORT_RUN_IT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+}  // namespace
+
+template <typename K>
+hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
+    constexpr int IT = RunKT<K>::IT;
+    if (run_it_knob() == 2 * IT) return merge_level_it<K, 2 * IT>(src, dst, n, lw, s, o0, o1);
+    return merge_level_it<K, IT>(src, dst, n, lw, s, o0, o1);
+}
+
+template hipError_t merge_level<uint32_t>(const uint32_t*, uint32_t*, int64_t, int, hipStream_t, int64_t,
+                                          int64_t);
+template hipError_t merge_level<uint64_t>(const uint64_t*, uint64_t*, int64_t, int, hipStream_t, int64_t,
+                                          int64_t);
+
+}  // namespace misort

@@ -1,0 +1,149 @@
+"""GPU parity of the merge levels (runs.hip) -- the passes that finish the
+local sort replacing the reference's std::sort (psort.cc:175) once runs leave
+the SORT tile.
+
+* One merge level (misort_pass_probe, kind run_merge) on inputs made of
+  ascending runs of 2^hi keys, ragged tails included, is compared bit for bit
+  with numpy: each pair of runs sorted.
+* Full local sorts under MISORT_MERGE_FROM / MISORT_MERGE_FROM_U64 (0: the
+  bitonic network only; later levels: network then merges) and the merge tile
+  knob MISORT_RUN_IT run in child processes (the planner knobs are read once
+  per process) against np.sort."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import misort  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+U32_T = torch.uint32 if hasattr(torch, "uint32") else torch.int32
+U64_T = torch.uint64 if hasattr(torch, "uint64") else torch.int64
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = misort.Context(0)
+    yield c
+    c.close()
+
+
+def runs_input(n, hi, dt, seed, dup=False):
+    rng = np.random.default_rng(seed)
+    top = 64 if dup else np.iinfo(dt).max
+    x = rng.integers(0, top, size=n, dtype=dt, endpoint=not dup)
+    if not dup:
+        x[::11] = np.iinfo(dt).max  # all-ones keys (the padding value) inside the data
+        x[5::13] = 0
+    w = 1 << hi
+    for s in range(0, n, w):
+        x[s:s + w].sort()
+    return x
+
+
+def expect(x, hi):
+    out = x.copy()
+    w2 = 2 << hi
+    for s in range(0, x.size, w2):
+        out[s:s + w2].sort()
+    return out
+
+
+def run_level(ctx, x, hi):
+    if x.dtype == np.uint32:
+        d_in = torch.from_numpy(x.view(np.int32)).cuda().view(U32_T)
+    else:
+        d_in = torch.from_numpy(x.view(np.int64)).cuda().view(U64_T)
+    d_out = torch.empty_like(d_in)
+    ctx.pass_probe(d_in, d_out, "run_merge", hi, 0, False, reps=1)
+    torch.cuda.synchronize()
+    if x.dtype == np.uint32:
+        return d_out.view(torch.int32).cpu().numpy().view(np.uint32)
+    return d_out.view(torch.int64).cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("dt", [np.uint32, np.uint64])
+@pytest.mark.parametrize("hi", [13, 15, 17])
+@pytest.mark.parametrize("n", [(1 << 19), (1 << 19) - 4097, (1 << 18) + 3, 5000, 12345])
+def test_merge_level_matches_numpy(ctx, dt, hi, n):
+    if dt == np.uint32 and hi < 13:
+        pytest.skip()
+    x = runs_input(n, hi, dt, n + hi)
+    np.testing.assert_array_equal(run_level(ctx, x, hi), expect(x, hi))
+
+
+@pytest.mark.parametrize("dt", [np.uint32, np.uint64])
+def test_merge_level_duplicates_and_single_run(ctx, dt):
+    # duplicate-heavy pairs, and n < 2^(hi+1) (one pair, ragged B) and n <= 2^hi (copy)
+    for n, hi in [(1 << 18, 14), (40000, 15), (30000, 15), (4096, 13)]:
+        x = runs_input(n, hi, dt, n, dup=True)
+        np.testing.assert_array_equal(run_level(ctx, x, hi), expect(x, hi))
+
+
+def test_merge_level_rejects_bad_shapes(ctx):
+    x = np.arange(1 << 16, dtype=np.uint32)
+    for hi in (5, 11):  # runs shorter than the merge tile
+        with pytest.raises(misort.MisortError):
+            run_level(ctx, x, hi)
+
+
+CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import misort
+n, kb = int(sys.argv[2]), int(sys.argv[3])
+ctx = misort.Context(0)
+plan = misort.plan(n, kb)
+rng = np.random.default_rng(n)
+dt = np.uint32 if kb == 4 else np.uint64
+keys = rng.integers(0, np.iinfo(dt).max, size=n, dtype=dt, endpoint=True)
+keys[: n // 5] = keys[n // 7]
+keys[n // 3: n // 3 + 999] = np.iinfo(dt).max
+if kb == 4:
+    T = torch.uint32 if hasattr(torch, "uint32") else torch.int32
+    d = torch.from_numpy(keys.view(np.int32)).cuda().view(T)
+else:
+    T = torch.uint64 if hasattr(torch, "uint64") else torch.int64
+    d = torch.from_numpy(keys.view(np.int64)).cuda().view(T)
+out = torch.empty_like(d)
+ctx.parallel_bitonic_sort(d, n, n, out=out)
+ctx.local_sort(d)  # in place (ping-pong through the context's scratch)
+torch.cuda.synchronize()
+iv = torch.int32 if kb == 4 else torch.int64
+a = out.view(iv).cpu().numpy().view(dt)
+b = d.view(iv).cpu().numpy().view(dt)
+ref = np.sort(keys)
+ok = np.array_equal(a, ref) and np.array_equal(b, ref)
+print("RUNS", sum(1 for p in plan if p[0] == "run_merge"), "OK" if ok else "MISMATCH")
+ctx.close()
+"""
+
+
+@pytest.mark.parametrize("kb,env,n", [
+    (4, {"MISORT_MERGE_FROM": "0"}, (1 << 22) + 4099),
+    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 22) + 4099),
+    (4, {"MISORT_MERGE_FROM": "19"}, 1 << 23),
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_IT": "32"}, (1 << 21) + 77),
+    (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),
+    (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 21) + 4099),
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_IT": "32"}, (1 << 20) + 5),
+])
+def test_full_sort_merge_from(kb, env, n):
+    r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
+                        str(kb)], env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
+    _, count, verdict = line.split()
+    assert verdict == "OK", line
+    m0 = int(next(iter(env.values())))
+    if m0 == 0:
+        assert int(count) == 0
+    else:
+        assert int(count) == max(0, (n - 1).bit_length() - m0)

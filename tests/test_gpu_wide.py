@@ -116,7 +116,7 @@ ctx.close()
 @pytest.mark.parametrize("wide", ["0", "1"])
 @pytest.mark.parametrize("n", [1 << 24, (1 << 23) + 4099])
 def test_full_sort_with_and_without_wide_passes(wide, n):
-    env = dict(os.environ, MISORT_WIDE=wide)
+    env = dict(os.environ, MISORT_WIDE=wide, MISORT_MERGE_FROM="0")  # the network path
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n)],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]

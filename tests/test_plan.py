@@ -14,6 +14,7 @@ import misort
 
 KIND_SORT, KIND_ROWS, KIND_MERGE, KIND_SPAN = "tile_sort", "global_pass", "tile_merge", "span_pass"
 KIND_WIDE = "wide_pass"  # ROWS stages in the 2^16-key register tile (u32)
+KIND_RUNS = "run_merge"  # one merge level (runs.hip): runs of 2^hi -> 2^(hi+1)
 
 
 def ceil_log2(n):
@@ -25,10 +26,23 @@ def network(k, lt):
     return [(m, b) for m in range(lt + 1, k + 1) for b in range(m - 1, -1, -1)]
 
 
+def split_runs(plan):
+    """(network passes, merge-level passes): merge levels come last."""
+    i = next((j for j, q in enumerate(plan) if q[0] == KIND_RUNS), len(plan))
+    assert all(q[0] == KIND_RUNS for q in plan[i:])
+    return plan[:i], plan[i:]
+
+
+def merge_from(plan, k):
+    """First level the merge passes finish (k + 1: none)."""
+    _, runs = split_runs(plan)
+    return runs[0][1] if runs else k
+
+
 def plan_stages(plan, lt):
-    """Stages the plan's passes run after the SORT pass, as (level, bit)."""
+    """Network stages the plan's passes run after the SORT pass, as (level, bit)."""
     out = []
-    for kind, hi, r, flip in plan[1:]:
+    for kind, hi, r, flip in split_runs(plan)[0][1:]:
         if kind in (KIND_ROWS, KIND_WIDE):
             # a ROWS pass runs bits hi..hi-R+1 of the level whose stages they are;
             # the level is known from the flip (hi = m-1) or from the sequence so far
@@ -68,6 +82,11 @@ def replay(keys, plan, lt):
             stage(x, m, b)
     for m, b in plan_stages(plan, lt):
         stage(x, m, b)
+    for kind, hi, _, _ in split_runs(plan)[1]:
+        # merge level: every run of 2^hi is sorted, each pair of runs is merged
+        runs = x.reshape(-1, 1 << hi)
+        assert np.all(runs[:, 1:] >= runs[:, :-1])
+        x = np.sort(x.reshape(-1, 1 << (hi + 1)), axis=1).reshape(-1)
     return x[: keys.size]
 
 
@@ -82,7 +101,9 @@ def test_plan_covers_network(n, key_bytes):
     p = misort.plan(n, key_bytes)
     assert p[0][0] == KIND_SORT
     k = ceil_log2(n)
-    assert plan_stages(p, lt) == network(k, lt)
+    m0 = merge_from(p, k)
+    assert plan_stages(p, lt) == network(min(k, max(m0, lt)), lt)
+    assert [q[1] for q in split_runs(p)[1]] == list(range(m0, k)) if m0 < k else True
     for kind, hi, r, flip in p[1:]:
         if kind in (KIND_ROWS, KIND_SPAN):
             assert 1 <= r <= lt - 5  # rows keep >= 32 consecutive keys (128 B for u32)
@@ -91,12 +112,14 @@ def test_plan_covers_network(n, key_bytes):
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + 28 passes with wide ROWS passes (1 + 29 without them;
-    # the level-by-level plan needs 1 + 35)
-    assert len(misort.plan(1 << 30, 4)) == 29
-    assert len(misort.plan(1 << 28, 4)) == 24
-    assert len(misort.plan(1 << 24, 4)) == 15
-    assert any(k == KIND_SPAN for k, *_ in misort.plan(1 << 30, 4))
+    # 2^30 u32: 1 SORT + one merge pass per level 16..30 (the network alone
+    # needs 1 + 28 with wide ROWS passes, 1 + 29 without, 1 + 35 level by level)
+    assert len(misort.plan(1 << 30, 4)) == 16
+    assert len(misort.plan(1 << 28, 4)) == 14
+    assert len(misort.plan(1 << 24, 4)) == 10
+    assert [q[0] for q in misort.plan(1 << 30, 4)] == [KIND_SORT] + [KIND_RUNS] * 15
+    # u64: 2^13-key SORT tiles, then merge levels
+    assert len(misort.plan((1 << 29) - 3, 8)) == 1 + 29 - 13
 
 
 @pytest.mark.parametrize("key_bytes", [4, 8])
@@ -130,7 +153,7 @@ def test_plans_with_and_without_wide_passes(wide):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sizes = [(1 << 16) + 3, 100003, (1 << 18) - 5, 1 << 20, 1 << 24, 1 << 28, 1 << 30, 1 << 31]
     r = subprocess.run([sys.executable, "-c", WIDE_CHILD, os.path.join(root, "parallel-computing-mpi_amd"),
-                        ",".join(map(str, sizes))], env=dict(os.environ, MISORT_WIDE=wide),
+                        ",".join(map(str, sizes))], env=dict(os.environ, MISORT_WIDE=wide, MISORT_MERGE_FROM="0"),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     plans = {int(k): [tuple(p) for p in v] for k, v in json.loads(r.stdout).items()}
@@ -150,3 +173,38 @@ def test_plans_with_and_without_wide_passes(wide):
         assert n_wide > 0 and len(plans[1 << 30]) <= 30
     else:
         assert n_wide == 0
+
+
+@pytest.mark.parametrize("mfrom", ["0", "15", "19", "23"])
+def test_plans_merge_from(mfrom):
+    """Network-then-merge plans under MISORT_MERGE_FROM (0: network only, the
+    pass counts of the pure network plan): the network part covers the network
+    up to the merge level, merge passes cover each remaining level once, and
+    small plans replay to a sort."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sizes = [(1 << 16) + 3, 100003, (1 << 18) - 5, 1 << 20, 1 << 24, 1 << 28, 1 << 30]
+    r = subprocess.run([sys.executable, "-c", WIDE_CHILD, os.path.join(root, "parallel-computing-mpi_amd"),
+                        ",".join(map(str, sizes))], env=dict(os.environ, MISORT_MERGE_FROM=mfrom),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plans = {int(k): [tuple(p) for p in v] for k, v in json.loads(r.stdout).items()}
+    lt = misort.tile_log2(4)
+    for n, p in plans.items():
+        k = ceil_log2(n)
+        m0 = merge_from(p, k)
+        if mfrom == "0":
+            assert m0 == k
+        else:
+            assert m0 == (int(mfrom) if int(mfrom) < k else k)
+        assert plan_stages(p, lt) == network(min(k, m0), lt)
+        if n <= 1 << 18:
+            rng = np.random.default_rng(n)
+            keys = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+            np.testing.assert_array_equal(replay(keys, p, lt), np.sort(keys))
+    if mfrom == "0":
+        # the pure network plan: 1 SORT + 28 passes at 2^30 (wide ROWS passes)
+        assert len(plans[1 << 30]) == 29 and len(plans[1 << 28]) == 24 and len(plans[1 << 24]) == 15

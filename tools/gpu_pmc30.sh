@@ -5,7 +5,7 @@ R="$GRAFT_REPO_ROOT"; cd /tmp && export TMPDIR=/tmp
 OUT="$R/gpurun_out/pmc30"; mkdir -p "$OUT"
 run() {  # name, counters...
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "k_stream|k_rows_wide" -d "$OUT/$name" -o $name --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-events > "$OUT/$name.log" 2>&1 || { echo "pass $name failed"; tail -3 "$OUT/$name.log"; return 1; }
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "k_stream|k_rows_wide|k_runs_" -d "$OUT/$name" -o $name --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-events > "$OUT/$name.log" 2>&1 || { echo "pass $name failed"; tail -3 "$OUT/$name.log"; return 1; }
   echo "pass $name ok"
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && python3 "$R/tools/traffic.py" "$OUT" > "$OUT/traffic.json" && cat "$OUT/traffic.json"

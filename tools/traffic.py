@@ -5,7 +5,12 @@ FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes
 of a 16-B-per-lane streaming read (MI355X_MICROARCH.md, HBM section; confirmed
 on this access shape by profiles/r01/pmc/calfetch_*), so it is doubled.
 Families follow the k_stream TileMode template argument (0 SORT, 1 MERGE, 2 ROWS, 3 SPAN);
-k_rows_wide (2^16-key register-tile ROWS) is its own family.
+k_rows_wide (2^16-key register-tile ROWS) is its own family.  The merge levels
+(runs.hip) are two launches per level: run_merge = k_runs_merge + k_runs_partition
+per level.  Their loads are 4 B per lane, not 16 B; FETCH_SIZE still reports half the bytes
+there (k_runs_merge reads every key exactly once: raw 2.197e9 vs 4.295e9 read
+at 2^30, profiles/r01/pmc30_v11/), so the same doubling applies.  The raw value
+is kept as "read_bytes_raw" and the factor as "fetch_scale".
     tools/traffic.py gpurun_out/pmc30 > profiles/traffic.json
 """
 import collections
@@ -27,16 +32,30 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
             fam = FAMILY[m.group(2)]
         elif "k_rows_wide" in name:
             fam = "wide_pass"
+        elif "k_runs_merge" in name:
+            fam = "run_merge_kernel"
+        elif "k_runs_partition" in name:
+            fam = "run_partition"
         else:
             continue
         acc[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {"source": os.path.basename(os.path.normpath(root)),
        "note": "bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE correction)"}
+SCALE = float(os.environ.get("RUN_FETCH_SCALE", "2"))  # 4-B-per-lane loads: see the docstring
 for fam, cs in acc.items():
-    f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2 if cs.get("FETCH_SIZE") else None
+    scale = SCALE if fam.startswith("run_") else 2.0
+    f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * scale if cs.get("FETCH_SIZE") else None
     w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024 if cs.get("WRITE_SIZE") else None
     out[fam] = {"launches": max(len(v) for v in cs.values()), "read_bytes_per_launch": f,
                 "write_bytes_per_launch": w,
-                "bytes_per_launch": (f + w) if f is not None and w is not None else None}
+                "bytes_per_launch": (f + w) if f is not None and w is not None else None,
+                "fetch_scale": scale,
+                "read_bytes_raw": f / scale if f is not None else None}
+if "run_merge_kernel" in out and "run_partition" in out:
+    a, b = out["run_merge_kernel"], out["run_partition"]
+    out["run_merge"] = {k: a[k] + b[k] for k in ("read_bytes_per_launch", "write_bytes_per_launch",
+                                                 "bytes_per_launch", "read_bytes_raw")}
+    out["run_merge"].update(launches=a["launches"], fetch_scale=SCALE)
+    out["run_merge"]["note"] = "per level: k_runs_merge + k_runs_partition"
 json.dump(out, sys.stdout, indent=1)
 print()
