@@ -74,6 +74,10 @@ struct PlanKnobs {
     // (0 = network only), per key type.  Measured at 2^30 u32 / 2^29 u64: the
     // SORT tile's level is best (profiles/r01/runs/).
     int merge_from_u32 = 15, merge_from_u64 = 13;
+    // u32 sorts of at most 2^merge_min_log2 keys (cache-resident: 2^24 u32 is
+    // 64 MiB) stay on the network, whose passes are shorter there (2^24:
+    // 0.60 vs 0.63 ms, 2^20: 0.18 vs 0.21 ms; 2^28: 10.3 vs 6.8 ms).
+    int merge_min_log2_u32 = 24;
     PlanKnobs();
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
@@ -1304,7 +1308,7 @@ template <typename K, int LT, int LTR>
 std::vector<Pass> plan_uncached(int k, bool runs) {
     const PlanKnobs& kn = plan_knobs();
     const int m0 = kn.merge_from((int)sizeof(K));
-    if (runs && m0 > 0 && k > m0) {
+    if (runs && m0 > 0 && k > m0 && !(sizeof(K) == 4 && k <= kn.merge_min_log2_u32)) {
         std::vector<Pass> ps = plan_uncached<K, LT, LTR>(m0 < LT ? LT : m0, false);
         for (int lw = m0 < LT ? LT : m0; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
         return ps;

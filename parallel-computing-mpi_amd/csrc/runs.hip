@@ -28,18 +28,19 @@ template <typename K>
 struct RunKT;
 template <>
 struct RunKT<uint32_t> {
-    static constexpr int IT = 16;  // 4096-key tiles, 16 KiB of LDS (IT 32: 1.56x slower)
+    static constexpr int IT = 16;
+    static constexpr int NT = 512;  // 8192-key tiles, 32 KiB of LDS (NT 256: -2 %, 1024: -8 %; IT 32: 1.5x slower)
     static constexpr int V = 4;
     typedef uint32_t vec __attribute__((ext_vector_type(4)));
 };
 template <>
 struct RunKT<uint64_t> {
-    static constexpr int IT = 16;  // 4096-key tiles, 32 KiB of LDS (IT 8: -2 %)
+    static constexpr int IT = 16;
+    static constexpr int NT = 256;  // 4096-key tiles, 32 KiB of LDS (IT 8: -2 %, NT 512: -7 %)
     static constexpr int V = 2;
     typedef uint64_t vec __attribute__((ext_vector_type(2)));
 };
 
-constexpr int RUN_NT = 256;
 
 template <typename K>
 constexpr K KT_MAX = (K)~(K)0;
@@ -71,10 +72,10 @@ __device__ int64_t run_corank(const K* __restrict__ A, int64_t na, const K* __re
     return lo;
 }
 
-template <typename K, int IT>
+template <typename K, int NT, int IT>
 __global__ void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, int64_t t0, int64_t ntiles,
                                  int64_t* __restrict__ co) {
-    constexpr int TILE = RUN_NT * IT;
+    constexpr int TILE = NT * IT;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ntiles) return;
     const int64_t g0 = (t0 + i) * TILE;
@@ -83,11 +84,11 @@ __global__ void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, i
     co[i] = run_corank(A, p.na, A + ((int64_t)1 << lw), p.nb, g0 - p.base);
 }
 
-template <typename K, int IT>
-__global__ __launch_bounds__(RUN_NT) void k_runs_merge(const K* __restrict__ src, K* __restrict__ dst,
+template <typename K, int NT, int IT>
+__global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K* __restrict__ dst,
                                                        int64_t n, int lw, int64_t t0,
                                                        const int64_t* __restrict__ co) {
-    constexpr int V = RunKT<K>::V, TILE = RUN_NT * IT;
+    constexpr int V = RunKT<K>::V, TILE = NT * IT;
     typedef typename RunKT<K>::vec vec;
     __shared__ __attribute__((aligned(16))) K s[TILE];
     const int tid = threadIdx.x;
@@ -107,12 +108,12 @@ __global__ __launch_bounds__(RUN_NT) void k_runs_merge(const K* __restrict__ src
         K x[IT];
 #pragma unroll
         for (int k = 0; k < IT; ++k) {
-            const int e = k * RUN_NT + tid;
+            const int e = k * NT + tid;
             const K* q = e < la ? A + e : B + (e - la);
             x[k] = e < len ? __builtin_nontemporal_load(q) : KT_MAX<K>;
         }
 #pragma unroll
-        for (int k = 0; k < IT; ++k) s[k * RUN_NT + tid] = x[k];
+        for (int k = 0; k < IT; ++k) s[k * NT + tid] = x[k];
     }
     __syncthreads();
 
@@ -157,11 +158,11 @@ __global__ __launch_bounds__(RUN_NT) void k_runs_merge(const K* __restrict__ src
     if (len == TILE) {
 #pragma unroll
         for (int k = 0; k < IT / V; ++k) {
-            const int e = (k * RUN_NT + tid) * V;
+            const int e = (k * NT + tid) * V;
             __builtin_nontemporal_store(*reinterpret_cast<const vec*>(s + e), reinterpret_cast<vec*>(out + e));
         }
     } else {
-        for (int k = tid; k < len; k += RUN_NT) out[k] = s[k];
+        for (int k = tid; k < len; k += NT) out[k] = s[k];
     }
 }
 
@@ -188,9 +189,9 @@ int64_t* corank_scratch(size_t bytes, hipStream_t s) {
     return (int64_t*)e.first;
 }
 
-template <typename K, int IT>
+template <typename K, int NT, int IT>
 hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
-    constexpr int TILE = RUN_NT * IT;
+    constexpr int TILE = NT * IT;
     if (o1 <= 0 || o1 > n) o1 = n;
     if (n <= 0 || o0 >= o1) return hipSuccess;
     if (lw < 12 || lw > 40 || ((int64_t)1 << lw) < TILE || src == dst || o0 < 0 || o0 % TILE ||
@@ -201,17 +202,23 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
     const int64_t nco = t0 + ntiles < (n + TILE - 1) / TILE ? ntiles + 1 : ntiles;
     int64_t* co = corank_scratch((size_t)(ntiles + 1) * sizeof(int64_t), s);
     if (!co) return hipErrorOutOfMemory;
-    k_runs_partition<K, IT><<<(unsigned)((nco + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
-    k_runs_merge<K, IT><<<(unsigned)ntiles, RUN_NT, 0, s>>>(src, dst, n, lw, t0, co);
+    k_runs_partition<K, NT, IT><<<(unsigned)((nco + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
+    k_runs_merge<K, NT, IT><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, co);
     return hipGetLastError();
 }
 
-// MISORT_RUN_IT: keys per lane of the merge tile (u32 16 or 32, u64 16 or 32).
+int env_knob(const char* k) {
+    const char* e = getenv(k);
+    return e ? atoi(e) : 0;
+}
+// MISORT_RUN_IT: keys per lane of the merge tile (u32 16 or 32, u64 16 or 32);
+// MISORT_RUN_NT: lanes per merge workgroup (256, 512 or 1024).
 int run_it_knob() {
-    static const int v = [] {
-        const char* e = getenv("MISORT_RUN_IT");
-        return e ? atoi(e) : 0;
-    }();
+    static const int v = env_knob("MISORT_RUN_IT");
+    return v;
+}
+int run_nt_knob() {
+    static const int v = env_knob("MISORT_RUN_NT");
     return v;
 }
 
@@ -219,9 +226,15 @@ int run_it_knob() {
 
 template <typename K>
 hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
-    constexpr int IT = RunKT<K>::IT;
-    if (run_it_knob() == 2 * IT) return merge_level_it<K, 2 * IT>(src, dst, n, lw, s, o0, o1);
-    return merge_level_it<K, IT>(src, dst, n, lw, s, o0, o1);
+    constexpr int IT = RunKT<K>::IT, NT = RunKT<K>::NT;
+    if (lw < 0 || lw > 40) return hipErrorInvalidValue;
+    if (run_it_knob() == 2 * IT) return merge_level_it<K, 256, 2 * IT>(src, dst, n, lw, s, o0, o1);
+    const bool fits = ((int64_t)1 << lw) >= 1024 * IT;  // runs no shorter than the largest tile
+    if (run_nt_knob() == 256) return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
+    if (run_nt_knob() == 512 && fits) return merge_level_it<K, 512, IT>(src, dst, n, lw, s, o0, o1);
+    if (run_nt_knob() == 1024 && fits) return merge_level_it<K, 1024, IT>(src, dst, n, lw, s, o0, o1);
+    if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1);
+    return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);  // runs shorter than the default tile
 }
 
 template hipError_t merge_level<uint32_t>(const uint32_t*, uint32_t*, int64_t, int, hipStream_t, int64_t,

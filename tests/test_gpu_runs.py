@@ -7,7 +7,7 @@ the SORT tile.
   with numpy: each pair of runs sorted.
 * Full local sorts under MISORT_MERGE_FROM / MISORT_MERGE_FROM_U64 (0: the
   bitonic network only; later levels: network then merges) and the merge tile
-  knob MISORT_RUN_IT run in child processes (the planner knobs are read once
+  knobs MISORT_RUN_IT / MISORT_RUN_NT run in child processes (the planner knobs are read once
   per process) against np.sort."""
 import os
 import subprocess
@@ -131,13 +131,17 @@ ctx.close()
     (4, {"MISORT_MERGE_FROM": "15"}, (1 << 22) + 4099),
     (4, {"MISORT_MERGE_FROM": "19"}, 1 << 23),
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_IT": "32"}, (1 << 21) + 77),
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "256"}, (1 << 21) + 77),
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
     (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),
     (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 21) + 4099),
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_IT": "32"}, (1 << 20) + 5),
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_NT": "512"}, (1 << 20) + 5),
 ])
 def test_full_sort_merge_from(kb, env, n):
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
-                        str(kb)], env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+                        str(kb)], env=dict(os.environ, MISORT_MERGE_MIN_LOG2="0", **env), capture_output=True,
+                       text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
     _, count, verdict = line.split()
