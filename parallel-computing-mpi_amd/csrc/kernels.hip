@@ -118,8 +118,20 @@ __global__ __launch_bounds__(MS_NT) void k_merge_tiles(const K* __restrict__ A, 
     const int64_t i0 = co[t], i1 = co[t + 1];
     const int64_t j0 = d0 + ds - i0, j1 = d0 + de - i1;
     const int la = (int)(i1 - i0), lb = (int)(j1 - j0), len = la + lb;
-    for (int k = threadIdx.x; k < la; k += MS_NT) s[k] = A[i0 + k];
-    for (int k = threadIdx.x; k < lb; k += MS_NT) s[la + k] = B[j0 + k];
+    // all MS_ITEMS loads of a lane are issued before the first LDS write (one
+    // memory latency per tile: the per-key loop waited out one per key)
+    {
+        K x[MS_ITEMS];
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k) {
+            const int e = k * MS_NT + threadIdx.x;
+            const K* q = e < la ? A + i0 + e : B + j0 + (e - la);
+            x[k] = e < len ? *q : (K)0;
+        }
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k)
+            if (k * MS_NT + (int)threadIdx.x < len) s[k * MS_NT + threadIdx.x] = x[k];
+    }
     __syncthreads();
     const int dk = threadIdx.x * MS_ITEMS < len ? threadIdx.x * MS_ITEMS : len;
     int lo = dk - lb > 0 ? dk - lb : 0, hi = dk < la ? dk : la;
