@@ -409,6 +409,12 @@ __device__ __forceinline__ void sort_levels_w(K* s, int t) {
 // 5.57 ms (all LDS; profiles/r01/ab/wave_levels.txt).  Default: levels 6..8 in
 // the wave (quad_perm / row_half_mirror only), 9..15 in LDS phases.
 // (Semantics of every cross-lane op: tools/dpp_probe.hip.)
+// Probe-only (tools/build_variant.sh): last level the u32 SORT pass's LDS
+// phases run (15 = the whole tile; smaller values time the tile's lower levels
+// and do not sort).
+#ifndef MISORT_SORT_TOP
+#define MISORT_SORT_TOP 15
+#endif
 #ifndef MISORT_WAVE_SORT
 #define MISORT_WAVE_SORT 1
 #endif
@@ -974,7 +980,7 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < m.ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
-        sort_levels_w<K, WL + 1, LT>(s, t);
+        sort_levels_w<K, WL + 1, MISORT_SORT_TOP>(s, t);
         final_store<K, LT, TM_SORT, SL, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n, FULL,
                                                                                          t);
         if constexpr (!PERSIST) break;

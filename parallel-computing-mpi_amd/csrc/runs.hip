@@ -35,8 +35,8 @@ struct RunKT<uint32_t> {
 };
 template <>
 struct RunKT<uint64_t> {
-    static constexpr int IT = 16;
-    static constexpr int NT = 256;  // 4096-key tiles, 32 KiB of LDS (IT 8: -2 %, NT 512: -7 %)
+    static constexpr int IT = 8;
+    static constexpr int NT = 1024;  // 8192-key tiles, 64 KiB of LDS (256 x 16: -4 %, 512 x 16: -11 %)
     static constexpr int V = 2;
     typedef uint64_t vec __attribute__((ext_vector_type(2)));
 };
@@ -211,7 +211,7 @@ int env_knob(const char* k) {
     const char* e = getenv(k);
     return e ? atoi(e) : 0;
 }
-// MISORT_RUN_IT: keys per lane of the merge tile (u32 16 or 32, u64 16 or 32);
+// MISORT_RUN_IT: keys per lane of the merge tile (16, 32 on 256 lanes, or 8 on 1024 lanes);
 // MISORT_RUN_NT: lanes per merge workgroup (256, 512 or 1024).
 int run_it_knob() {
     static const int v = env_knob("MISORT_RUN_IT");
@@ -229,6 +229,8 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
     constexpr int IT = RunKT<K>::IT, NT = RunKT<K>::NT;
     if (lw < 0 || lw > 40) return hipErrorInvalidValue;
     if (run_it_knob() == 2 * IT) return merge_level_it<K, 256, 2 * IT>(src, dst, n, lw, s, o0, o1);
+    if (run_it_knob() == IT / 2 && ((int64_t)1 << lw) >= 1024 * (IT / 2))
+        return merge_level_it<K, 1024, IT / 2>(src, dst, n, lw, s, o0, o1);  // same tile, half the keys per lane
     const bool fits = ((int64_t)1 << lw) >= 1024 * IT;  // runs no shorter than the largest tile
     if (run_nt_knob() == 256) return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
     if (run_nt_knob() == 512 && fits) return merge_level_it<K, 512, IT>(src, dst, n, lw, s, o0, o1);
