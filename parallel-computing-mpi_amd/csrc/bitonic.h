@@ -412,6 +412,11 @@ __device__ __forceinline__ void sort_levels_w(K* s, int t) {
 // Probe-only (tools/build_variant.sh): last level the u32 SORT pass's LDS
 // phases run (15 = the whole tile; smaller values time the tile's lower levels
 // and do not sort).
+// Build-time variant: first level of the u32 SORT tile done as an LDS merge
+// (0: the bitonic network for every level; see tile_merge_levels).
+#ifndef MISORT_SORT_MERGE_FROM
+#define MISORT_SORT_MERGE_FROM 0
+#endif
 #ifndef MISORT_SORT_TOP
 #define MISORT_SORT_TOP 15
 #endif
@@ -931,6 +936,48 @@ __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* i
     }
 }
 
+// Levels L0..LT of the u32 SORT tile as merges in LDS (build-time variant,
+// MISORT_SORT_MERGE_FROM = L0): before level L the tile holds ascending runs of
+// 2^(L-1) keys at s[pad(v)]; lane t writes outputs [32t, 32t + 32) of its pair's
+// merge -- a co-rank search, 32 serial LDS reads, then (after a barrier) 32
+// LDS writes.  The final store's register stages then act on sorted data, where
+// a half-cleaner changes nothing.
+template <int L, int LT>
+__device__ __forceinline__ void tile_merge_levels(uint32_t* s, int t) {
+    if constexpr (L <= LT) {
+        constexpr int W = 1 << (L - 1);
+        const int v0 = t << 5;
+        const int base = (v0 >> L) << L, d = v0 - base;
+        const int bb = base + W;
+        int lo = d > W ? d - W : 0, hi = d < W ? d : W;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s[pad(base + mid)] <= s[pad(bb + d - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        int ia = lo, ib = d - lo;
+        uint32_t av = s[pad(base + (ia < W ? ia : 0))], bv = s[pad(bb + (ib < W ? ib : 0))];
+        uint32_t r[32];
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+            const bool takeA = ia < W && (ib >= W || av <= bv);
+            r[c] = takeA ? av : bv;
+            ia += takeA;
+            ib += !takeA;
+            const int nx = takeA ? base + (ia < W ? ia : 0) : bb + (ib < W ? ib : 0);
+            const uint32_t x = s[pad(nx)];
+            av = takeA ? x : av;
+            bv = takeA ? bv : x;
+        }
+        __syncthreads();
+        const int a0 = pad(v0);
+#pragma unroll
+        for (int c = 0; c < 32; ++c) s[a0 + c] = r[c];
+        __syncthreads();
+        tile_merge_levels<L + 1, LT>(s, t);
+    }
+}
+
 template <bool PERSIST, bool FULL>
 __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, TileMap m,
                                                       int64_t tile0) {
@@ -980,7 +1027,12 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < m.ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
-        sort_levels_w<K, WL + 1, MISORT_SORT_TOP>(s, t);
+        if constexpr (MISORT_SORT_MERGE_FROM > WL) {
+            sort_levels_w<K, WL + 1, MISORT_SORT_MERGE_FROM - 1>(s, t);
+            tile_merge_levels<MISORT_SORT_MERGE_FROM, LT>(s, t);
+        } else {
+            sort_levels_w<K, WL + 1, MISORT_SORT_TOP>(s, t);
+        }
         final_store<K, LT, TM_SORT, SL, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n, FULL,
                                                                                          t);
         if constexpr (!PERSIST) break;
