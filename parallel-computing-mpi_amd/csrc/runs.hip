@@ -21,6 +21,14 @@
 #include <map>
 #include <mutex>
 
+// Build-time A/B switches (tools/build_variant.sh): non-temporal tile loads / stores.
+#ifndef MISORT_RUN_NT_LOAD
+#define MISORT_RUN_NT_LOAD 1
+#endif
+#ifndef MISORT_RUN_NT_STORE
+#define MISORT_RUN_NT_STORE 1
+#endif
+
 namespace misort {
 namespace {
 
@@ -110,7 +118,11 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
         for (int k = 0; k < IT; ++k) {
             const int e = k * NT + tid;
             const K* q = e < la ? A + e : B + (e - la);
+#if MISORT_RUN_NT_LOAD
             x[k] = e < len ? __builtin_nontemporal_load(q) : KT_MAX<K>;
+#else
+            x[k] = e < len ? *q : KT_MAX<K>;
+#endif
         }
 #pragma unroll
         for (int k = 0; k < IT; ++k) s[k * NT + tid] = x[k];
@@ -159,7 +171,11 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
 #pragma unroll
         for (int k = 0; k < IT / V; ++k) {
             const int e = (k * NT + tid) * V;
+#if MISORT_RUN_NT_STORE
             __builtin_nontemporal_store(*reinterpret_cast<const vec*>(s + e), reinterpret_cast<vec*>(out + e));
+#else
+            *reinterpret_cast<vec*>(out + e) = *reinterpret_cast<const vec*>(s + e);
+#endif
         }
     } else {
         for (int k = tid; k < len; k += NT) out[k] = s[k];

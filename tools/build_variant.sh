@@ -10,6 +10,7 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$HERE/include -I$C $2"
 /opt/rocm/bin/hipcc $F -c "$C/sort_u32.hip" -o "$O/sort_u32.o" &
 /opt/rocm/bin/hipcc $F -c "$C/sort_u64.hip" -o "$O/sort_u64.o" &
 /opt/rocm/bin/hipcc $F -c "$C/kernels.hip" -o "$O/kernels.o" &
+/opt/rocm/bin/hipcc $F -c "$C/runs.hip" -o "$O/runs.o" &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$L/variants/libmisort_$1.so" "$O/kernels.o" "$O/sort_u32.o" "$O/sort_u64.o" "$L/codec.o" "$L/runs.o" "$L/runtime.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$L/variants/libmisort_$1.so" "$O/kernels.o" "$O/sort_u32.o" "$O/sort_u64.o" "$L/codec.o" "$O/runs.o" "$L/runtime.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf "$O"
