@@ -11,21 +11,27 @@ Total keys are fixed (strong scaling).  Keys: counter-based SplitMix64
 (seed 0x5EED0003), top 32 bits, generated on the GPU outside the timed region;
 the sort is out of place so every step sorts the same unsorted input.
 
+`--gpus N` without a torchrun environment (no WORLD_SIZE) relaunches this file
+under `python -m torch.distributed.run --nproc-per-node N` as a child process
+BEFORE anything touches the GPU, and exits with the child's status.
+
 Rank 0 prints ONE JSON line with the metric, the per-kernel roofline of the
 dominant kernel (HIP events on the sort stream inside the timed region;
 algorithmic bytes = 2 * keys * 4 B per pass) and the CPU baseline: the
 reference's own parallel_bitonic_sort (oracle/_ref, compiled from the
-unmodified psort.cc) under mpirun on this host's cores, on a bounded sample.
+unmodified psort.cc) under mpirun on this host's cores, on the same workload.
+At N > 1 it adds per-stage exchange / merge-split times, the xGMI bytes and
+rate of every hypercube stage, and t1 / (P * tP) against a 1-GPU leg of the
+same keys run in the same job.
 """
 import argparse
 import json
 import os
 import re
+import socket
 import subprocess
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "parallel-computing-mpi_amd"))
@@ -37,6 +43,55 @@ REF_BIN = os.path.join(ROOT, "oracle", "_ref", "psort_ref")
 MPIRUN = "/opt/conda/bin/mpirun"
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--logn", type=int, default=30, help="log2 of the total key count")
+    ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
+    ap.add_argument("--algo", choices=["bitonic", "sample"], default="bitonic",
+                    help="bitonic = psort.cc:167 (the metric); sample = psort.cc:203-375 redesigned")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N>1: skip the extra sample-sort timing reported under 'alt'")
+    ap.add_argument("--no-t1", action="store_true",
+                    help="N>1: skip the 1-GPU leg that scaling_eff is computed against")
+    ap.add_argument("--cpu-sample-logn", type=int, default=None,
+                    help="log2 keys of the CPU baseline sample (default: the workload, --logn)")
+    ap.add_argument("--cpu-sweep", action="store_true",
+                    help="also time the reference at P = 1, 2, 4, ... cores on u32 and on its own f64 "
+                         "workload (BASELINE.md section 3), reported under cpu_sweep")
+    ap.add_argument("--cpu-sweep-logn", type=int, default=27)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="time without per-launch HIP events (roofline omitted)")
+    ap.add_argument("--host-io", action="store_true",
+                    help="also time the PCIe-inclusive path (host keys -> misort_sort_host -> host "
+                         "keys), staged and overlapped vs one chunk; reported under 'host_io', "
+                         "never as value")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, gpus, port):
+    """The torchrun command that runs this file as `gpus` ranks (one per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def needs_launch(args, env=None):
+    env = os.environ if env is None else env
+    return args.gpus > 1 and "WORLD_SIZE" not in env
+
+
+# ------------------------------------------------------------- CPU baseline
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -48,39 +103,115 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(sample_logn, cores):
-    """The reference sorter's parallel_bitonic_sort on host cores (mpirun)."""
-    n = 1 << sample_logn
-    sample = (f"2^{sample_logn} u32 keys (SplitMix64 seed {SEED:#x}, the bench workload's "
-              f"generator), reference psort.cc parallel_bitonic_sort on doubles via "
-              f"oracle/_ref harness, mpirun -np {cores}, CPU: {cpu_model()}")
-    if os.path.exists(REF_BIN) and os.path.exists(MPIRUN):
-        cmd = [MPIRUN, "-np", str(cores), REF_BIN, "--dtype", "u32", "--gen-splitmix", hex(SEED),
-               "--n", str(n)]
-        try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
-            m = re.search(r'"sort_s": ([0-9.eE+-]+)', r.stdout)
-            errs = re.search(r"(\d+) errors in sorting", r.stdout)
-            if r.returncode == 0 and m:
-                t = float(m.group(1))
-                return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": cores,
-                        "kind": "reference", "sample": sample, "sort_s": t,
-                        "errors": int(errs.group(1)) if errs else None}
-            sys.stderr.write(f"cpu baseline failed ({r.returncode}): {r.stderr[-400:]}\n")
-        except (subprocess.TimeoutExpired, OSError) as e:
-            sys.stderr.write(f"cpu baseline failed: {e}\n")
-    # Fallback: the C restatement (single thread) on a smaller sample.
+def cpu_share():
+    """CPUs this process may use: affinity mask, cgroup quota, MISORT_CPU_CORES."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = f"sched_getaffinity={n}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                cg = max(1, int(int(q) / int(per)))
+                why += f", cgroup cpu.max={cg}"
+                n = min(n, cg)
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("MISORT_CPU_CORES"):
+        n = int(os.environ["MISORT_CPU_CORES"])
+        why += f", MISORT_CPU_CORES={n}"
+    return max(1, n), why
+
+
+def pow2_floor(n):
+    p = 1
+    while p * 2 <= n:
+        p *= 2
+    return p
+
+
+def run_reference(cmd, timeout):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"{' '.join(cmd[:4])}...: rc {r.returncode}: {r.stderr[-400:]}")
+    return r.stdout
+
+
+def ref_keys_time(logn, cores, dtype="u32"):
+    """Reference parallel_bitonic_sort on SplitMix keys (our harness around the
+    unmodified psort.cc); returns (sort seconds, errors)."""
+    out = run_reference([MPIRUN, "-np", str(cores), REF_BIN, "--dtype", dtype, "--gen-splitmix",
+                         hex(SEED), "--n", str(1 << logn)], timeout=900)
+    m = re.search(r'"sort_s": ([0-9.eE+-]+)', out)
+    errs = re.search(r"(\d+) errors in sorting", out)
+    return float(m.group(1)), int(errs.group(1)) if errs else None
+
+
+def ref_psort_time(logn, cores):
+    """The reference binary's own run (`mpirun -np P psort N`, its generator,
+    its doubles, its printed max-over-ranks parallel sort time)."""
+    out = run_reference([MPIRUN, "-np", str(cores), REF_BIN, str(1 << logn)], timeout=900)
+    m = re.search(r"parallel sort time = ([0-9.eE+-]+)", out)
+    errs = re.search(r"(\d+) errors in sorting", out)
+    return float(m.group(1)), int(errs.group(1)) if errs else None
+
+
+def cpu_baseline(sample_logn, sweep, sweep_logn):
+    """The reference sorter's parallel_bitonic_sort on this host's cores."""
+    share, why = cpu_share()
+    cores = pow2_floor(share)
+    model = cpu_model()
+    if not (os.path.exists(REF_BIN) and os.path.exists(MPIRUN)):
+        # Loud: the reference harness is built in the build container
+        # (__graft_entry__.build(), oracle/Makefile) and travels in-tree.
+        msg = (f"cpu baseline: {REF_BIN} or {MPIRUN} missing -- falling back to the C restatement "
+               f"(kind 'port', 1 thread); rebuild with __graft_entry__.build() where /root/reference exists")
+        sys.stderr.write("WARNING " + msg + "\n")
+        return port_baseline(min(sample_logn, 24), msg)
+    res = {"unit": "Gkeys/s", "cores": cores, "kind": "reference",
+           "cores_why": f"largest power of two <= CPUs available ({why}); psort.cc needs 2^d ranks",
+           "cpu": model}
+    try:
+        t, errs = ref_keys_time(sample_logn, cores)
+        res.update(value=(1 << sample_logn) / t / 1e9, sort_s=t, errors=errs,
+                   sample=(f"2^{sample_logn} u32 keys (SplitMix64 seed {SEED:#x}, the bench workload) "
+                           f"carried as doubles through the reference psort.cc parallel_bitonic_sort "
+                           f"(oracle/_ref harness), mpirun -np {cores}; timed region psort.cc:633-653, "
+                           f"max over ranks"))
+    except (RuntimeError, subprocess.TimeoutExpired, OSError, AttributeError) as e:
+        sys.stderr.write(f"WARNING cpu baseline failed: {e}\n")
+        return port_baseline(min(sample_logn, 24), f"reference run failed: {e}")
+    if sweep:
+        rows = []
+        p = 1
+        while p <= cores:
+            row = {"p": p}
+            try:
+                tu, eu = ref_keys_time(sweep_logn, p)
+                tf, ef = ref_psort_time(sweep_logn, p)
+                row.update(u32_s=tu, u32_gkeys=(1 << sweep_logn) / tu / 1e9, u32_errors=eu,
+                           f64_s=tf, f64_gkeys=(1 << sweep_logn) / tf / 1e9, f64_errors=ef)
+            except (RuntimeError, subprocess.TimeoutExpired, OSError, AttributeError) as e:
+                row["error"] = str(e)[-200:]
+            rows.append(row)
+            p *= 2
+        res["sweep"] = {"n": 1 << sweep_logn, "rows": rows,
+                        "note": "u32: SplitMix keys as doubles through parallel_bitonic_sort; f64: the "
+                                "reference binary's own generator and stdout time (bitonic swapped in)"}
+    return res
+
+
+def port_baseline(logn, why):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
-    n = 1 << min(sample_logn, 24)
+    n = 1 << logn
     x = O.splitmix(SEED, n, np.uint32)
     t0 = time.perf_counter()
     O.parallel_bitonic_sort(x, 1)
     t = time.perf_counter() - t0
     return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": 1, "kind": "port",
-            "sample": f"2^{min(sample_logn, 24)} u32 keys, oracle/oracle.c restatement, 1 thread",
-            "sort_s": t}
+            "sample": f"2^{logn} u32 keys, oracle/oracle.c restatement, 1 thread", "sort_s": t,
+            "fallback_reason": why}
 
 
 def load_traffic():
@@ -92,53 +223,47 @@ def load_traffic():
         return json.load(f)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--logn", type=int, default=30, help="log2 of the total key count")
-    ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
-    ap.add_argument("--algo", choices=["bitonic", "sample"], default="bitonic",
-                    help="bitonic = psort.cc:167 (the metric); sample = psort.cc:203-375 redesigned")
-    ap.add_argument("--no-alt", action="store_true",
-                    help="N>1: skip the extra sample-sort timing reported under 'alt'")
-    ap.add_argument("--cpu-sample-logn", type=int, default=27)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-events", action="store_true",
-                    help="time without per-launch HIP events (roofline omitted)")
-    ap.add_argument("--host-io", action="store_true",
-                    help="also time the PCIe-inclusive path (host keys -> misort_sort_host -> host "
-                         "keys), staged and overlapped vs one chunk; reported under 'host_io', "
-                         "never as value")
-    args = ap.parse_args()
+# -------------------------------------------------------------------- ranks
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if needs_launch(args):
+        # one process per GPU; this process never touches the GPU
+        cmd = launch_command(argv, args.gpus, free_port())
+        return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        sys.stderr.write(f"WARNING --gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks\n")
 
-    # The CPU baseline runs first, before this process touches the GPU.
+    # The CPU baseline runs first, before this process touches the GPU
+    # (rank 0 at N = 1 only).
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = 1
-        while cores * 2 <= min(os.cpu_count() or 1, 16):
-            cores *= 2
-        cpu = cpu_baseline(args.cpu_sample_logn, cores)
+        cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
+                           args.cpu_sweep, args.cpu_sweep_logn)
 
+    import numpy as np
     import torch
     import torch.distributed as dist
     import misort
 
     if world > 1:
         dist.init_process_group("gloo")  # host plumbing only: ids, barriers, max
-    torch.cuda.set_device(local_rank)
-    ctx = misort.Context(local_rank)
+    ndev = torch.cuda.device_count()
+    shared = world > ndev  # several ranks on one GPU: RCCL over sockets (correctness mode)
+    dev = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev)
+    ctx = misort.Context(dev)
     if world > 1:
-        ctx.comm_init_torch()
+        ctx.comm_init_torch(share_gpu=shared)
+    nranks = ctx.numprocs  # the ranks RCCL actually saw
 
     n_total = 1 << args.logn
-    sizes = misort.block_sizes(n_total, world)
-    loc, max_size = sizes[rank], n_total // world + 1
+    sizes = misort.block_sizes(n_total, nranks)
+    loc, max_size = sizes[rank], n_total // nranks + 1
     g0 = sum(sizes[:rank])
     kdt = (torch.uint32 if hasattr(torch, "uint32") else torch.int32) if args.dtype == "u32" else \
           (torch.uint64 if hasattr(torch, "uint64") else torch.int64)
@@ -159,8 +284,11 @@ def main():
         else:
             ctx.parallel_bitonic_sort(d_in, loc, max_size, out=d_out, stream=stream.cuda_stream)
 
-    def step():
-        run(args.algo)
+    def max_over_ranks(v):
+        t = torch.tensor([v], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     def timed(algo, steps):
         """warm, then barrier + sync around `steps` sorts; max over ranks (s)."""
@@ -173,13 +301,10 @@ def main():
             run(algo)
         torch.cuda.synchronize()
         barrier()
-        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        return float(tt.item())
+        return max_over_ranks(time.perf_counter() - t0)
 
     for _ in range(args.warmup):
-        step()
+        run(args.algo)
     torch.cuda.synchronize()
     ctx.exchange_stats()  # reset
     events = not args.no_kernel_events
@@ -190,21 +315,38 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run(args.algo)
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     kern = ctx.profile_read() if events else {}
+    nst = len(misort.schedule(nranks, rank))
+    stages = ctx.profile_stages(nst) if events and nranks > 1 and args.algo == "bitonic" else []
     ctx.profile(False)
     xst = ctx.exchange_stats()
-
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
     errors = ctx.check_sort(d_out, loc)  # psort.cc:497-520 over all ranks
+
+    stage_rows = None
+    if stages:
+        sched = misort.schedule(nranks, rank)
+        d = int(np.log2(nranks))
+        ij = [(i, j) for i in range(d) for j in range(i, -1, -1)]  # psort.cc:184-185
+        stage_rows = []
+        for st, (cnt, xms, mms, byt) in enumerate(stages):
+            cnt = max(cnt, 1)
+            x_max = max_over_ranks(xms / cnt)
+            m_max = max_over_ranks(mms / cnt)
+            b_max = max_over_ranks(byt / cnt)
+            stage_rows.append({
+                "stage": st, "i": ij[st][0], "j": ij[st][1], "partner_bit": ij[st][1],
+                "rank0_partner": sched[st][0],
+                "exchange_ms_max": x_max, "merge_split_ms_max": m_max,
+                "exchange_bytes_max": b_max,
+                # bytes one rank sends + receives over its links in the stage / stage time
+                "xgmi_GBs": b_max / (x_max * 1e-3) / 1e9 if x_max > 0 else None})
+
     alt = None
-    if world > 1 and args.algo == "bitonic" and not args.no_alt:
+    if nranks > 1 and args.algo == "bitonic" and not args.no_alt:
         # the redesigned sample sort (one RCCL all-to-all) on the same input, same contract
         ts = timed("sample", args.steps)
         alt = {"sample_sort": {"value": n_total * args.steps / ts / 1e9, "unit": "Gkeys/s",
@@ -212,6 +354,30 @@ def main():
                                "check_errors": ctx.check_sort(d_out, loc),
                                "note": "psort.cc:203-375 redesigned: samples, one all-to-all-v, "
                                        "merge tree, rebalance to the reference layout"}}
+
+    t1 = None
+    if nranks > 1 and not args.no_t1:
+        # 1-GPU leg: rank 0 sorts ALL n_total keys alone on its GPU (a P = 1
+        # context), same keys, same steps; scaling_eff = t1 / (P * tP)
+        barrier()
+        if rank == 0:
+            solo = misort.Context(dev)
+            a = torch.empty(n_total, dtype=kdt, device="cuda")
+            b = torch.empty_like(a)
+            solo.fill_splitmix(a, SEED, 0)
+            for _ in range(2):
+                solo.parallel_bitonic_sort(a, n_total, n_total, out=b, stream=stream.cuda_stream)
+            torch.cuda.synchronize()
+            ts0 = time.perf_counter()
+            for _ in range(args.steps):
+                solo.parallel_bitonic_sort(a, n_total, n_total, out=b, stream=stream.cuda_stream)
+            torch.cuda.synchronize()
+            t1 = (time.perf_counter() - ts0) / args.steps
+            assert solo.check_sort(b) == 0
+            del a, b
+            solo.close()
+            torch.cuda.empty_cache()
+        barrier()
 
     host_io = None
     if args.host_io:
@@ -228,10 +394,8 @@ def main():
                 t0 = time.perf_counter()
                 h_out = ctx.sort_host(h_in, max_size, out=h_buf)
                 barrier()
-                tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-                if world > 1:
-                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                best = float(tt.item()) if best is None else min(best, float(tt.item()))
+                tt = max_over_ranks(time.perf_counter() - t0)
+                best = tt if best is None else min(best, tt)
             res[name] = {"value": n_total / best / 1e9, "unit": "Gkeys/s", "ms": best * 1e3,
                          "chunk_keys": chunk}
             assert bool(np.all(h_out[1:] >= h_out[:-1])) if loc > 1 else True
@@ -242,11 +406,13 @@ def main():
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
+        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys) + merge-path HBM levels "
+                      "(the reference's local std::sort, psort.cc:175)")
         out = {
             "metric": METRIC,
             "value": n_total * args.steps / elapsed / 1e9,
             "unit": "Gkeys/s",
-            "n_gpus": world,
+            "n_gpus": nranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms,
@@ -258,25 +424,34 @@ def main():
             "config": {"workload": f"bitonic sort 2^{args.logn} {args.dtype} keys "
                                    f"(BASELINE config {'3/4' if args.logn == 30 else 'custom'})",
                        "keys": n_total, "keys_per_gpu": loc,
-                       "algo": args.algo,
-                       "parallelism": (f"hypercube bitonic, {world} GPU(s), RCCL compare-split"
+                       "algo": args.algo, "local_sort": local_algo,
+                       "parallelism": (f"hypercube bitonic, {nranks} GPU(s), RCCL compare-split"
                                        if args.algo == "bitonic" else
-                                       f"sample sort, {world} GPU(s), RCCL all-to-all")},
+                                       f"sample sort, {nranks} GPU(s), RCCL all-to-all")},
             "check_errors": errors,
         }
-        if world > 1:
+        if shared:
+            out["shared_gpu"] = ("several ranks on one GPU: RCCL over its socket transport "
+                                 "(NCCL_HOSTID per rank) -- a correctness run, not an xGMI figure")
+        if nranks > 1:
             out["exchange"] = {"stages_per_step": xst[0] / args.steps,
                                "rank0_bytes_per_step": xst[1] / args.steps,
                                "rank0_whole_block_bytes_per_step": xst[2] / args.steps}
+            if stage_rows:
+                out["exchange"]["stages"] = stage_rows
+        if t1 is not None:
+            out["t1_ms"] = t1 * 1e3
+            out["scaling_eff"] = t1 / (nranks * elapsed / args.steps)
         if kern:
             per = {}
             for name, (nl, tms, byt) in kern.items():
                 if nl:
                     per[name] = {"launches_per_step": nl / args.steps, "ms_per_step": tms / args.steps,
                                  "avg_launch_us": tms / nl * 1e3,
-                                 "achieved_GBs": byt / (tms * 1e-3) / 1e9 if tms > 0 else None}
+                                 "achieved_GBs": byt / (tms * 1e-3) / 1e9 if tms > 0 and byt > 0 else None}
             out["kernels"] = per
-            dom = max(kern.items(), key=lambda kv: kv[1][1])
+            hbm = {k: v for k, v in kern.items() if k != "exchange"}
+            dom = max(hbm.items(), key=lambda kv: kv[1][1])
             name, (nl, tms, byt) = dom
             traffic = load_traffic()
             tr = None
@@ -287,7 +462,7 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                                "traffic": tr, "algorithmic_bytes_per_launch": byt / nl,
                                "avg_launch_us": tms / nl * 1e3}
-            kt = sum(v[1] for v in kern.values()) / args.steps
+            kt = sum(v[1] for k, v in hbm.items()) / args.steps
             out["kernel_ms_per_step"] = kt
         if alt:
             out["alt"] = alt
@@ -298,7 +473,8 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

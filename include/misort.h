@@ -55,7 +55,9 @@ enum misort_kernel_kind {
     MISORT_K_OTHER = 4,
     MISORT_K_SPAN = 5,        /* tail of one level + head of the next    */
     MISORT_K_WIDE = 6,        /* ROWS strides in a 2^16-key register tile */
-    MISORT_K_RUN_MERGE = 7    /* one merge level: runs 2^hi -> 2^(hi+1)  */
+    MISORT_K_RUN_MERGE = 7,   /* one merge level: runs 2^hi -> 2^(hi+1)  */
+    MISORT_K_EXCHANGE = 8     /* compare-split exchange leg (splitter samples, RCCL
+                                 send/recv, codec), device time between events */
 };
 
 typedef struct misort_ctx misort_ctx;
@@ -104,10 +106,14 @@ int64_t misort_block_size(int64_t n, int p, int rank);
  * rank's block (capacity >= loc_size); on return it holds the rank's block of
  * the result -- the same block the reference leaves in its returned buffer,
  * including the reference's output for uneven blocks.  max_size bounds every
- * rank's block (psort.cc:557, the MPI_Sendrecv receive capacity).  Blocking
- * for the host only at the start (one size exchange); the rest is enqueued on
- * `stream`.  Steps: local sort (psort.cc:175) then d(d+1)/2 rounds of RCCL
- * send/recv with the partner plus a device merge-split. */
+ * rank's block (psort.cc:557, the MPI_Sendrecv receive capacity); it is checked
+ * collectively (every rank against the smallest max_size, so all ranks fail
+ * together), and max_size <= 0 means the largest block.  Steps: local sort
+ * (psort.cc:175) then d(d+1)/2 rounds of RCCL send/recv with the partner plus a
+ * device merge-split.  At P = 1 everything is enqueued on `stream`; at P > 1
+ * the host waits on the stream at the start (size exchange) and 1-3 times per
+ * stage (splitter samples to the host, and for delta-coded messages the coded
+ * size and the size handshake), the rest is enqueued. */
 int misort_parallel_bitonic_sort(misort_ctx* ctx, int dtype, void* d_keys, int64_t loc_size,
                                  int64_t max_size, void* stream);
 /* Same, out of place: d_in is left unchanged, d_out receives the block
@@ -224,6 +230,13 @@ int misort_profile_reset(misort_ctx* ctx);
  * summed device time (ms) and summed algorithmic HBM bytes. */
 int misort_profile_read(misort_ctx* ctx, int kind, int64_t* launches, double* total_ms,
                         double* bytes);
+
+/* Per hypercube stage of misort_parallel_bitonic_sort (stage 0 .. d(d+1)/2-1,
+ * the order of psort.cc:184-185), summed over the profiled sorts: number of
+ * sorts, exchange-leg device time (ms), merge-split kernel time (ms) and the
+ * bytes this rank sent plus received in the stage. */
+int misort_profile_stage(misort_ctx* ctx, int stage, int64_t* count, double* exchange_ms,
+                         double* merge_ms, double* exchange_bytes);
 
 /* log2 of the LDS tile (keys) used for a key width of 4 or 8 bytes. */
 int misort_tile_log2(int key_bytes);

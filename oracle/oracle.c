@@ -78,6 +78,34 @@ void orc_splitmix_u64(uint64_t seed, int64_t g0, int64_t cnt, uint64_t *out) {
         out[k] = splitmix_at(seed, g0 + k);
 }
 
+void orc_u64mix(uint64_t seed, int64_t n, int64_t g0, int64_t cnt, uint64_t top, uint64_t *out) {
+    /* draws below `top` (all-ones: the full 64-bit range below it) */
+    const uint64_t lim = top;
+    uint64_t x = lcg_skip(1ULL << 32, (uint64_t)g0); /* ODD_DIST stream at g0 */
+    for (int64_t k = 0; k < cnt; ++k) {
+        int64_t g = g0 + k;
+        x = (LCG_A * x + LCG_C) & LCG_MASK;
+        uint64_t h = splitmix_at(seed, g), v = splitmix_at(seed ^ 0xA5A5A5A5A5A5A5A5ULL, g);
+        uint32_t c = (uint32_t)(h >> 32) % 100u;
+        uint64_t key;
+        if (c < 40) {
+            key = splitmix_at(seed + 1, (int64_t)(v & 1023)) % lim;
+        } else if (c < 70) { /* psort.cc:600-609 at index g */
+            unsigned short ctr = (unsigned short)((g + 1) & 0xFFFF);
+            double val = pow(ldexp((double)x, -48), 1.0 + 3 * ((double)ctr / (double)n));
+            val = val * val;
+            memcpy(&key, &val, 8);
+        } else if (c < 90) {
+            key = v % lim;
+        } else if (c < 95) {
+            key = 0;
+        } else {
+            key = top;
+        }
+        out[k] = key;
+    }
+}
+
 /* -------------------------------------------------------------- local sort */
 
 /* psort.cc:175 std::sort.  Keys carry no payload, so any correct ascending sort

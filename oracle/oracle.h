@@ -34,6 +34,16 @@ void orc_generate_f64(int64_t n, int64_t g0, int64_t cnt, double *out);
 void orc_splitmix_u32(uint64_t seed, int64_t g0, int64_t cnt, uint32_t *out);
 void orc_splitmix_u64(uint64_t seed, int64_t g0, int64_t cnt, uint64_t *out);
 
+/* BASELINE config-5 key mix (not in the reference):
+ * per global index g, counter-based on seed: 40 % from a 1024-value alphabet
+ * (duplicate-heavy), 30 % the bit patterns of the reference's own ODD_DIST
+ * doubles (psort.cc:587-609 at index g of an n-key sequence: skewed), 20 %
+ * uniform, 5 % zeros, 5 % `top` (the sentinel: all-ones for the full mix;
+ * 0x7FF0000000000000 for the variant the reference can carry as ordered
+ * doubles, with alphabet/uniform keys then drawn below it).  Independent of
+ * how the index range is split, so rank blocks can be generated alone. */
+void orc_u64mix(uint64_t seed, int64_t n, int64_t g0, int64_t cnt, uint64_t top, uint64_t *out);
+
 /* psort.cc:175 -- ascending local sort (std::sort). f64 compares as double. */
 void orc_sort(int dtype, void *keys, int64_t n);
 

@@ -185,6 +185,12 @@ static int keys_mode(int argc, char** argv) {
     std::vector<long long> sizes(numprocs);
     MPI_Gather(&oloc, 1, MPI_LONG_LONG, sizes.data(), 1, MPI_LONG_LONG, 0, MPI_COMM_WORLD);
     if (!out.empty()) {
+        if (myid == 0) {  // truncate once, before any rank writes its slice
+            int tfd = open(out.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+            if (tfd < 0) { perror(out.c_str()); MPI_Abort(MPI_COMM_WORLD, 2); }
+            close(tfd);
+        }
+        MPI_Barrier(MPI_COMM_WORLD);
         std::vector<unsigned char> ob((size_t)oloc * w + 8);
         for (long long k = 0; k < oloc; ++k) {
             if (w == 4) { uint32_t v = (uint32_t)res[k]; memcpy(&ob[k * 4], &v, 4); }

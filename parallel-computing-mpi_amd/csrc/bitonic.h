@@ -1478,7 +1478,9 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);  // runs of 2^hi -> 2^(hi+1)
-    if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER) return hipErrorInvalidValue;
+    if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER ||
+        kind == KIND_EXCHANGE)
+        return hipErrorInvalidValue;
     if (kind == KIND_GLOBAL || kind == KIND_SPAN) {
         if (R < 1 || R > LT - 5 || hi - R + 1 < LT - R || ((int64_t)1 << (hi + 1)) > ((int64_t)1 << ceil_log2(n)))
             return hipErrorInvalidValue;

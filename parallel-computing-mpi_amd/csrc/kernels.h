@@ -18,7 +18,8 @@ enum Kind : int {
     KIND_SPAN = 5,        // tail of one level + head of the next, row tile
     KIND_WIDE = 6,        // ROWS strides in a 2^16-key register tile (u32)
     KIND_RUNS = 7,        // one merge level: runs of 2^hi keys -> runs of 2^(hi+1)
-    KIND_COUNT = 8
+    KIND_EXCHANGE = 8,    // compare-split exchange leg (samples, RCCL send/recv, codec); not a kernel
+    KIND_COUNT = 9
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with

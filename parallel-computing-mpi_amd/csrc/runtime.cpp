@@ -67,12 +67,19 @@ struct Profiler final : misort::LaunchHook {
         int kind;
         hipEvent_t a, b;
         double bytes;
+        int stage;  // hypercube stage of parallel_sort (-1: local sort / other)
     };
+    static constexpr int MAX_STAGES = 64;
     std::vector<hipEvent_t> pool;
     std::vector<Rec> pending;
     int64_t launches[misort::KIND_COUNT] = {};
     double ms[misort::KIND_COUNT] = {};
     double bytes[misort::KIND_COUNT] = {};
+    // per hypercube stage: [0] exchange leg, [1] merge-split kernels
+    int64_t st_count[MAX_STAGES] = {};
+    double st_ms[MAX_STAGES][2] = {};
+    double st_bytes[MAX_STAGES] = {};
+    int stage = -1;
     Rec cur{};
     bool on = false;
 
@@ -87,7 +94,7 @@ struct Profiler final : misort::LaunchHook {
         return e;
     }
     void before(misort::Kind k, double b, hipStream_t s) override {
-        cur = Rec{k, take(), take(), b};
+        cur = Rec{k, take(), take(), b, stage};
         if (cur.a) (void)hipEventRecord(cur.a, s);
     }
     void after(misort::Kind, hipStream_t s) override {
@@ -104,6 +111,14 @@ struct Profiler final : misort::LaunchHook {
             launches[r.kind] += 1;
             ms[r.kind] += t;
             bytes[r.kind] += r.bytes;
+            if (r.stage >= 0 && r.stage < MAX_STAGES) {
+                const bool xg = r.kind == misort::KIND_EXCHANGE;
+                st_ms[r.stage][xg ? 0 : 1] += t;
+                if (xg) {
+                    st_count[r.stage] += 1;
+                    st_bytes[r.stage] += r.bytes;
+                }
+            }
             if (r.a) pool.push_back(r.a);
             if (r.b) pool.push_back(r.b);
         }
@@ -114,6 +129,9 @@ struct Profiler final : misort::LaunchHook {
         std::fill(std::begin(launches), std::end(launches), 0);
         std::fill(std::begin(ms), std::end(ms), 0.0);
         std::fill(std::begin(bytes), std::end(bytes), 0.0);
+        std::fill(std::begin(st_count), std::end(st_count), 0);
+        std::fill(&st_ms[0][0], &st_ms[0][0] + 2 * MAX_STAGES, 0.0);
+        std::fill(std::begin(st_bytes), std::end(st_bytes), 0.0);
     }
     ~Profiler() override {
         for (auto& r : pending) {
@@ -617,17 +635,29 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sb
 int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
                   int64_t max_size, hipStream_t s, const misort::StageIO* io = nullptr) {
     if (!valid_dtype(dtype)) return fail(MISORT_E_INVALID, "bad dtype %d", dtype);
-    if (loc < 0 || max_size < loc) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld",
-                                               (long long)loc, (long long)max_size);
+    if (loc < 0) return fail(MISORT_E_INVALID, "negative loc_size %lld", (long long)loc);
     const int p = c->nranks;
     if (p & (p - 1)) return fail(MISORT_E_NOT_POW2, "bitonic sort requires 2^d processors");
     int rc;
-    std::vector<int64_t> sizes(1, loc);
-    if (p > 1 && (rc = c->tr->allgather_i64(&loc, 1, sizes, s))) return rc;
+    // (loc, max_size) of every rank.  The capacity check is collective: every
+    // rank tests every block against the smallest max_size, so all ranks fail
+    // together instead of some entering the exchange alone.  max_size <= 0
+    // means "the largest block" (the reference's N/P+1 bound, psort.cc:557).
+    const int64_t mine[2] = {loc, max_size};
+    std::vector<int64_t> lm(mine, mine + 2);
+    if (p > 1 && (rc = c->tr->allgather_i64(mine, 2, lm, s))) return rc;
+    std::vector<int64_t> sizes(p);
+    int64_t cap = INT64_MAX, big = 0;
+    for (int r = 0; r < p; ++r) {
+        sizes[r] = lm[2 * r];
+        big = std::max(big, sizes[r]);
+        if (lm[2 * r + 1] > 0) cap = std::min(cap, lm[2 * r + 1]);
+    }
+    if (cap == INT64_MAX) cap = big;
     for (int r = 0; r < p; ++r)
-        if (sizes[r] > max_size)
+        if (sizes[r] > cap)
             return fail(MISORT_E_CAPACITY, "rank %d holds %lld keys > max_size %lld", r,
-                        (long long)sizes[r], (long long)max_size);
+                        (long long)sizes[r], (long long)cap);
     int partner[64], keep[64];
     const int nst = misort_bitonic_schedule(p, c->rank, partner, keep);
     const size_t w = key_bytes(dtype);
@@ -656,7 +686,23 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s, io ? &lio : nullptr))) return rc;
     if (chunk_out) return MISORT_OK;
     void* other = (cur == work) ? out : work;
+    misort::LaunchHook* hk = hook(c);
+    struct StageMark {  // attributes profiled launches to the hypercube stage
+        Profiler& pr;
+        StageMark(Profiler& p_, int st) : pr(p_) { pr.stage = st; }
+        ~StageMark() { pr.stage = -1; }
+    };
     for (int st = 0; st < nst; ++st) {
+        StageMark mark(c->prof, st);
+        if (hk) hk->before(misort::KIND_EXCHANGE, 0.0, s);
+        bool xg_open = hk != nullptr;
+        auto xg_close = [&](double bytes) {
+            if (xg_open) {
+                c->prof.cur.bytes = bytes;
+                hk->after(misort::KIND_EXCHANGE, s);
+                xg_open = false;
+            }
+        };
         const int q = partner[st];
         const int64_t nq = sizes[q];
         const bool mx = keep[st] != 0;  // this rank keeps the upper part
@@ -696,6 +742,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         if (k == 0) {  // no key crosses: both blocks stay as they are
             // relay units are 4 bytes on every rank of the stage (coded messages are words)
             if (relayed && (rc = relay_exchange(c, 4, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
+            xg_close(0.0);
             continue;
         }
         // A sends its top k = A[na-k, na); B sends its bottom k = B[0, k)
@@ -713,7 +760,10 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             nrecv = k;
         }
         const void* rkeys = c->recv.p;
-        if (k > 0 && c->compress) {
+        const int64_t moved0 = c->xchg_bytes;
+        // the codec's offsets and word totals are 32-bit: messages that could
+        // reach 2^32 words go raw (both sides decide from k alone)
+        if (k > 0 && c->compress && misort::codec_max_words(k, (int)w) < ((int64_t)1 << 32)) {
             // delta-code the sorted run; each side sends whichever of coded and raw is
             // smaller, and the receiver tells them apart by size (coded < raw)
             if ((rc = coded_exchange(c, dtype, q, relayed, sbuf, k, &rkeys, s))) return rc;
@@ -724,6 +774,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             c->xchg_bytes += (int64_t)(sbytes + rbytes);
             c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
         }
+        xg_close((double)(c->xchg_bytes - moved0));
         if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
         std::swap(cur, other);
     }
@@ -831,8 +882,8 @@ constexpr int kSamplesPerRank = 1024;
 int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc, int64_t max_size,
                     hipStream_t s) {
     if (!valid_dtype(dtype)) return fail(MISORT_E_INVALID, "bad dtype %d", dtype);
-    if (loc < 0 || max_size < loc) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld",
-                                               (long long)loc, (long long)max_size);
+    if (loc < 0 || (max_size > 0 && max_size < loc))
+        return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld", (long long)loc, (long long)max_size);
     const int p = c->nranks, me = c->rank;
     const size_t w = key_bytes(dtype);
     const bool f64 = dtype == MISORT_F64;
@@ -1490,8 +1541,8 @@ int misort_sort_host(misort_ctx* c, int dtype, const void* h_in, void* h_out, in
                      int64_t max_size) {
     if (!c || !valid_dtype(dtype) || loc < 0 || (loc > 0 && (!h_in || !h_out)))
         return fail(MISORT_E_INVALID, "bad sort_host arguments");
-    if (loc > max_size) return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld", (long long)loc,
-                                    (long long)max_size);
+    if (max_size > 0 && loc > max_size)
+        return fail(MISORT_E_INVALID, "loc_size %lld > max_size %lld", (long long)loc, (long long)max_size);
     const size_t w = key_bytes(dtype);
     const int64_t ch = stage_chunk(dtype);
     int rc = c->host_keys.ensure(std::max<size_t>((size_t)std::max<int64_t>(loc, 1) * w, 64));
@@ -1574,6 +1625,18 @@ int misort_profile_read(misort_ctx* c, int kind, int64_t* launches, double* tota
     if (launches) *launches = c->prof.launches[kind];
     if (total_ms) *total_ms = c->prof.ms[kind];
     if (bytes) *bytes = c->prof.bytes[kind];
+    return MISORT_OK;
+}
+
+int misort_profile_stage(misort_ctx* c, int stage, int64_t* count, double* exchange_ms, double* merge_ms,
+                         double* exchange_bytes) {
+    if (!c || stage < 0 || stage >= Profiler::MAX_STAGES) return fail(MISORT_E_INVALID, "bad stage");
+    int rc = c->prof.collect();
+    if (rc) return rc;
+    if (count) *count = c->prof.st_count[stage];
+    if (exchange_ms) *exchange_ms = c->prof.st_ms[stage][0];
+    if (merge_ms) *merge_ms = c->prof.st_ms[stage][1];
+    if (exchange_bytes) *exchange_bytes = c->prof.st_bytes[stage];
     return MISORT_OK;
 }
 

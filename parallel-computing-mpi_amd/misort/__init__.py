@@ -19,12 +19,12 @@ import os
 __all__ = [
     "U32", "U64", "F64", "MisortError", "NotPowerOfTwo", "NativeLibraryMissing",
     "library_path", "lib", "Context", "Group", "block_sizes", "schedule", "tile_log2", "plan",
-    "sample_indices", "exchange_count",
+    "sample_indices", "exchange_count", "set_shared_gpu_env",
 ]
 
 U32, U64, F64 = 0, 1, 2
 KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other", "span_pass",
-              "wide_pass", "run_merge"]
+              "wide_pass", "run_merge", "exchange"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.environ.get("MISORT_LIBRARY") or os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
@@ -87,6 +87,8 @@ def lib():
         "misort_profile_read": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_tile_log2": ([i32], i32),
+        "misort_profile_stage": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], i32),
         "misort_plan": ([ctypes.c_int64, i32, ctypes.POINTER(i32), i32], i32),
         "misort_pass_probe": ([vp, i32, vp, vp, i64, i32, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_float)], i32),
         "misort_group_create": ([i32, ctypes.POINTER(vp)], i32),
@@ -150,6 +152,13 @@ def exchange_count(samples_min, n_min, samples_max, n_max):
     dt = U32 if a.dtype == np.uint32 else U64
     return int(lib().misort_exchange_count(dt, a.ctypes.data_as(ctypes.c_void_p), n_min,
                                            b.ctypes.data_as(ctypes.c_void_p), n_max))
+
+
+def set_shared_gpu_env(rank):
+    """RCCL environment for ranks that share one GPU (see Context.comm_init_torch);
+    call before the first RCCL call of the process."""
+    os.environ["NCCL_HOSTID"] = f"misort-shared-gpu-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 
 
 def tile_log2(key_bytes):
@@ -264,10 +273,21 @@ class Context:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         _check(lib().misort_comm_init(self._h, nranks, rank, buf))
 
-    def comm_init_torch(self, group=None):
-        """Create the RCCL communicator; the id travels over torch.distributed."""
+    def comm_init_torch(self, group=None, share_gpu=None):
+        """Create the RCCL communicator; the id travels over torch.distributed.
+
+        share_gpu (default: env MISORT_SHARE_GPU=1): several ranks drive ONE
+        GPU.  RCCL refuses two ranks on one device within a host, so each rank
+        then presents its own host id (NCCL_HOSTID) and the ranks talk over
+        RCCL's socket transport on loopback: the RCCL calls, schedule and
+        merge-split are the production ones, the bandwidth is not xGMI's (a
+        correctness mode for 1-GPU boxes, never a performance figure)."""
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
+        if share_gpu is None:
+            share_gpu = os.environ.get("MISORT_SHARE_GPU", "0") == "1"
+        if share_gpu and world > 1:
+            set_shared_gpu_env(rank)
         obj = [self.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
         self.comm_init(world, rank, obj[0])
@@ -287,7 +307,7 @@ class Context:
         reference's hypercube schedule; returns the tensor holding the result
         (``buffer`` itself, or ``out`` when given: input left unchanged)."""
         loc = buffer.numel() if loc_buf_size is None else int(loc_buf_size)
-        mx = loc if max_size is None else int(max_size)
+        mx = 0 if max_size is None else int(max_size)  # 0: the largest block (collective)
         dt = _dtype_of(buffer)
         if out is None:
             _check(lib().misort_parallel_bitonic_sort(self._h, dt, _ptr(buffer), loc, mx,
@@ -316,7 +336,7 @@ class Context:
         layout, out of place (``out`` defaults to a new tensor)."""
         import torch
         loc = buffer.numel() if loc_buf_size is None else int(loc_buf_size)
-        mx = loc if max_size is None else int(max_size)
+        mx = 0 if max_size is None else int(max_size)
         out = torch.empty_like(buffer) if out is None else out
         _check(lib().misort_parallel_sample_sort(self._h, _dtype_of(buffer), _ptr(buffer), _ptr(out), loc, mx,
                                                  self._stream(stream)))
@@ -358,7 +378,7 @@ class Context:
             out = np.empty_like(arr)
         elif out.dtype != arr.dtype or out.size < arr.size or not out.flags.c_contiguous:
             raise ValueError("out must be a contiguous array of the input dtype and size")
-        mx = arr.size if max_size is None else int(max_size)
+        mx = 0 if max_size is None else int(max_size)
         _check(lib().misort_sort_host(self._h, dt, arr.ctypes.data_as(ctypes.c_void_p),
                                       out.ctypes.data_as(ctypes.c_void_p), arr.size, mx))
         return out
@@ -422,6 +442,16 @@ class Context:
                                        inp.numel() if n is None else n, k, hi, r, int(flip), reps,
                                        ctypes.byref(ms)))
         return ms.value
+
+    def profile_stages(self, nstages):
+        """Per hypercube stage: [(sorts, exchange_ms, merge_ms, exchange_bytes)]."""
+        res = []
+        for st in range(nstages):
+            n, xm, mm, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            _check(lib().misort_profile_stage(self._h, st, ctypes.byref(n), ctypes.byref(xm),
+                                              ctypes.byref(mm), ctypes.byref(b)))
+            res.append((int(n.value), float(xm.value), float(mm.value), float(b.value)))
+        return res
 
     def profile_read(self):
         """{kind: (launches, total_ms, algorithmic_bytes)}."""

@@ -5,8 +5,13 @@
 //
 // Same command line, same generator (erand48 + ODD_DIST, psort.cc:587-614),
 // same block layout (psort.cc:556-562), same six stdout lines and the same
-// check_sort count (psort.cc:497-520) as the reference run with its bitonic
-// sort.  What changes is behind the sort entry point: each MPI rank drives one
+// check_sort count (psort.cc:497-520) as the reference binary.  As shipped the
+// reference calls parallel_quick_sort (psort.cc:647-648), so that is the
+// default here too; --algo bitonic runs parallel_bitonic_sort (psort.cc:167),
+// the hot path this build accelerates (for N % P not in {0, 1} the bitonic
+// sort leaves the reference's deterministic boundary defects, so its error
+// count differs from the quick sort's).  What changes is behind the sort entry
+// point: each MPI rank drives one
 // GPU, keys are sorted in HBM by libmisort (gfx950 kernels) and the
 // compare-split exchange runs over RCCL/xGMI instead of MPI_Sendrecv.  MPI is
 // kept only for process bootstrap, the generator's seed hand-off, timing
@@ -17,12 +22,18 @@
 // reported separately with --verbose.
 //
 // Extensions (not in the reference; off by default):
-//   --algo bitonic|quick              bitonic (default, psort.cc:167) or the
-//                                     binary's shipped parallel_quick_sort
-//                                     (psort.cc:377; data-dependent block sizes)
+//   --algo quick|bitonic              quick (default: the binary's shipped
+//                                     parallel_quick_sort, psort.cc:377,
+//                                     data-dependent block sizes) or bitonic
+//                                     (psort.cc:167)
 //   --keys FILE --dtype u32|u64|f64   sort a raw little-endian key file
 //   --out FILE                        write the rank-ordered result
 //   --verbose                         extra timing lines on stderr
+//
+// More ranks than GPUs (e.g. mpirun -np 4 on a 1-GPU box): ranks share GPUs
+// round-robin.  RCCL refuses two ranks of one host on one device, so each rank
+// then presents its own NCCL_HOSTID and RCCL runs over its socket transport
+// (loopback): same calls, same results, not xGMI bandwidth.
 #include <mpi.h>
 
 #include <fcntl.h>
@@ -84,7 +95,7 @@ static double get_timer() {
         }                                                                           \
     } while (0)
 
-static bool g_quick = false;
+static bool g_quick = true;  // psort.cc:647-648 calls parallel_quick_sort
 
 static void misort_ok(int rc, const char* what) {
     if (rc == MISORT_E_NOT_POW2) {  // psort.cc:168-172 / 378-382
@@ -142,15 +153,37 @@ int main(int argc, char** argv) {
     long long input_size = 1024;  // psort.cc:538
     std::string keys_file, out_file, dtype_s = "f64";
     bool verbose = false;
-    if (argc == 2) input_size = atoll(argv[1]);  // psort.cc:541-544
-    for (int a = 1; a < argc && argc > 2; ++a) {
+    // psort.cc:541-544 takes argv[1] as N; here the one positional argument is N
+    // wherever it stands, so extension flags never read as the key count.
+    for (int a = 1; a < argc; ++a) {
         std::string s = argv[a];
-        if (s == "--keys" && a + 1 < argc) keys_file = argv[++a];
-        else if (s == "--out" && a + 1 < argc) out_file = argv[++a];
-        else if (s == "--dtype" && a + 1 < argc) dtype_s = argv[++a];
+        auto value = [&]() -> std::string {
+            if (a + 1 >= argc) {
+                if (myid == 0) fprintf(stderr, "psort: %s needs a value\n", s.c_str());
+                MPI_Abort(MPI_COMM_WORLD, 2);
+            }
+            return argv[++a];
+        };
+        if (s == "--keys") keys_file = value();
+        else if (s == "--out") out_file = value();
+        else if (s == "--dtype") dtype_s = value();
         else if (s == "--verbose") verbose = true;
-        else if (s == "--algo" && a + 1 < argc) g_quick = std::string(argv[++a]) == "quick";
-        else if (s[0] != '-') input_size = atoll(s.c_str());
+        else if (s == "--algo") {
+            const std::string v = value();
+            if (v != "quick" && v != "bitonic") {
+                if (myid == 0) fprintf(stderr, "psort: --algo quick|bitonic\n");
+                MPI_Abort(MPI_COMM_WORLD, 2);
+            }
+            g_quick = v == "quick";
+        } else if (!s.empty() && s[0] != '-') input_size = atoll(s.c_str());
+        else {
+            if (myid == 0) fprintf(stderr, "psort: unknown option %s\n", s.c_str());
+            MPI_Abort(MPI_COMM_WORLD, 2);
+        }
+    }
+    if (dtype_s != "u32" && dtype_s != "u64" && dtype_s != "f64") {
+        if (myid == 0) fprintf(stderr, "psort: --dtype u32|u64|f64\n");
+        MPI_Abort(MPI_COMM_WORLD, 2);
     }
     const int dtype = dtype_s == "u32" ? MISORT_U32 : dtype_s == "u64" ? MISORT_U64 : MISORT_F64;
     const size_t w = dtype == MISORT_U32 ? 4 : 8;
@@ -178,6 +211,16 @@ int main(int argc, char** argv) {
     HIP_OK(hipGetDeviceCount(&ndev));
     const char* dev_env = getenv("PSORT_DEVICE");
     const int dev = dev_env ? atoi(dev_env) : myid % std::max(1, ndev);
+    if (numprocs > std::max(1, ndev) && !dev_env) {
+        // GPUs shared by ranks: one host id per rank, RCCL over loopback sockets
+        char hid[64];
+        snprintf(hid, sizeof hid, "psort-shared-gpu-rank%d", myid);
+        setenv("NCCL_HOSTID", hid, 1);
+        setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+        if (myid == 0 && verbose)
+            fprintf(stderr, "psort: %d ranks on %d GPU(s): RCCL over sockets (correctness mode)\n", numprocs,
+                    ndev);
+    }
     misort_ctx* ctx = nullptr;
     misort_ok(misort_create(dev, &ctx), "misort_create");
     if (numprocs > 1) {
@@ -253,6 +296,17 @@ int main(int argc, char** argv) {
         HIP_OK(hipStreamSynchronize(st));
         t_d2h = MPI_Wtime() - t_d2h;
         if (!out_file.empty()) {
+            // one truncation (rank 0) before any rank writes its slice: a
+            // longer stale file must not keep its tail
+            if (myid == 0) {
+                int tfd = open(out_file.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+                if (tfd < 0) {
+                    perror(out_file.c_str());
+                    MPI_Abort(MPI_COMM_WORLD, 2);
+                }
+                close(tfd);
+            }
+            MPI_Barrier(MPI_COMM_WORLD);
             int ofd = open(out_file.c_str(), O_WRONLY | O_CREAT, 0644);
             if (ofd < 0 || (out_size > 0 &&
                             pwrite(ofd, host.data(), (size_t)out_size * w, (off_t)(out_off * (long long)w)) !=

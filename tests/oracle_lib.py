@@ -33,6 +33,7 @@ def lib():
         L.orc_generate_f64.argtypes = [i64, i64, i64, vp]
         L.orc_splitmix_u32.argtypes = [ctypes.c_uint64, i64, i64, vp]
         L.orc_splitmix_u64.argtypes = [ctypes.c_uint64, i64, i64, vp]
+        L.orc_u64mix.argtypes = [ctypes.c_uint64, i64, i64, i64, ctypes.c_uint64, vp]
         L.orc_sort.argtypes = [ctypes.c_int, vp, i64]
         L.orc_compare_split.argtypes = [ctypes.c_int, vp, i64, vp, i64, vp, ctypes.c_int]
         L.orc_parallel_bitonic_sort.argtypes = [ctypes.c_int, vp, i64, ctypes.c_int]
@@ -75,6 +76,18 @@ def splitmix(seed, n, dtype=np.uint32, g0=0):
         lib().orc_splitmix_u32(seed, g0, n, _ptr(out))
     else:
         lib().orc_splitmix_u64(seed, g0, n, _ptr(out))
+    return out
+
+
+ALL_ONES = 0xFFFFFFFFFFFFFFFF
+REF_TOP = 0x7FF0000000000000  # largest u64 the reference carries as an ordered double
+
+
+def u64mix(seed, n, top=ALL_ONES, g0=0, cnt=None):
+    """BASELINE config-5 mix (oracle.h orc_u64mix), keys [g0, g0+cnt) of n."""
+    cnt = n - g0 if cnt is None else cnt
+    out = np.empty(cnt, dtype=np.uint64)
+    lib().orc_u64mix(seed, n, g0, cnt, top, _ptr(out))
     return out
 
 

@@ -1,10 +1,15 @@
 """The psort drop-in binary (parallel-computing-mpi_amd/bin/psort) run as the
-reference is run, `mpirun -np 1 ./psort N`: the stable stdout lines (all but
+reference is run, `mpirun -np P ./psort N`: the stable stdout lines (all but
 the two timings) and the sorted output must equal the compiled reference's
-(golden fixtures), for the bitonic sort and for the shipped quick sort.  One
-rank only: the box has one GPU and RCCL refuses two ranks on one device (the
-multi-rank path is covered through misort.Group in test_gpu_multirank.py and
-test_gpu_quick.py)."""
+(golden fixtures), for the shipped quick sort (the default, psort.cc:647) and
+for the bitonic sort (--algo bitonic).
+
+P > 1 on a one-GPU box: the ranks share the GPU and psort switches RCCL to its
+socket transport (one NCCL_HOSTID per rank), so the full multi-rank binary --
+MPI bootstrap, generator seed offsets, block layout, RCCL communicator,
+compare-split exchanges, check_sort, rank-ordered --out file -- runs against the
+fixtures.  The key-file extension (--keys/--dtype/--out) is checked against the
+reference's keys fixtures."""
 import hashlib
 import json
 import os
@@ -22,7 +27,10 @@ PSORT = os.path.join(ROOT, "parallel-computing-mpi_amd", "bin", "psort")
 GOLD_DIR = os.path.join(ROOT, "tests", "golden")
 with open(os.path.join(GOLD_DIR, "golden.json")) as f:
     GOLD = json.load(f)["cases"]
-CASES = [c for c in GOLD if c["mode"] == "psort" and c["p"] == 1 and c["n"] <= 65537]
+CASES = [c for c in GOLD if c["mode"] == "psort" and
+         ((c["p"] == 1 and c["n"] <= 65537) or (c["p"] > 1 and c["n"] in (1031, 1000003, 1000005)))]
+KEYS = [c for c in GOLD if c["mode"] == "keys" and c["name"] in ("u32_n4099", "u64mix_n5003")]
+ENV = dict(os.environ, NCCL_SOCKET_IFNAME="lo")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -31,15 +39,59 @@ def binary():
         pytest.skip("psort binary or mpirun not present")
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c.get('algo', 'bitonic')}_N{c['n']}")
+def psort(p, *args, timeout=180):
+    r = subprocess.run([O.MPIRUN, "-np", str(p), PSORT, *args], capture_output=True, text=True,
+                       timeout=timeout, env=ENV)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    return r.stdout.strip().splitlines()
+
+
+def stable(lines):
+    return [l for l in lines if "required" not in l and "sort time" not in l]
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c.get('algo', 'bitonic')}_N{c['n']}_P{c['p']}")
 def test_psort_binary_matches_reference(case, tmp_path):
     out = tmp_path / "out.f64"
-    cmd = [O.MPIRUN, "-np", "1", PSORT, str(case["n"]), "--out", str(out),
-           "--algo", case.get("algo", "bitonic")]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
-    lines = r.stdout.strip().splitlines()
-    stable = [l for l in lines if "required" not in l and "sort time" not in l]
-    assert stable == case["stdout_stable"]
+    lines = psort(case["p"], str(case["n"]), "--out", str(out), "--algo", case.get("algo", "bitonic"))
+    assert stable(lines) == case["stdout_stable"]
     y = np.fromfile(out)
+    assert hashlib.sha256(y.tobytes()).hexdigest() == case["out_sha256"]
+
+
+def test_psort_default_is_the_shipped_quick_sort(tmp_path):
+    # psort.cc:647-648 calls parallel_quick_sort: no --algo = quick
+    case = [c for c in GOLD if c["mode"] == "psort" and c.get("algo") == "quick" and c["p"] == 1
+            and c["n"] == 1031][0]
+    out = tmp_path / "out.f64"
+    lines = psort(1, "1031", "--out", str(out))
+    assert stable(lines) == case["stdout_stable"]
+    assert hashlib.sha256(np.fromfile(out).tobytes()).hexdigest() == case["out_sha256"]
+
+
+def test_psort_flag_only_keeps_default_n():
+    # a lone extension flag is not the key count (psort.cc:538: N defaults to 1024)
+    lines = psort(1, "--verbose")
+    assert "generating input sequence consisting of 1024 doubles." in lines
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("p", [1, 2, 4])
+@pytest.mark.parametrize("algo", ["bitonic", "quick"])
+@pytest.mark.parametrize("name", ["u32_n4099", "u64mix_n5003"])
+def test_psort_key_files(name, algo, p, tmp_path):
+    case = [c for c in KEYS if c["name"] == name and c["p"] == p and c.get("algo", "bitonic") == algo][0]
+    if case["dtype"] == "u32":
+        keys = O.splitmix(0x5EED0001, case["n"], np.uint32)
+    else:
+        keys = np.fromfile(os.path.join(GOLD_DIR, f"keys_{name}.in"), dtype=np.uint64)
+    kf, of = tmp_path / "keys.bin", tmp_path / "out.bin"
+    keys.tofile(kf)
+    # a longer stale output file must not keep its tail (O_TRUNC)
+    np.full(case["n"] * 2, 7, dtype=keys.dtype).tofile(of)
+    lines = psort(p, "--keys", str(kf), "--dtype", case["dtype"], "--out", str(of), "--algo", algo)
+    assert f"{case['errors']} errors in sorting" in lines
+    y = np.fromfile(of, dtype=keys.dtype)
+    assert y.size == case["n"]
     assert hashlib.sha256(y.tobytes()).hexdigest() == case["out_sha256"]

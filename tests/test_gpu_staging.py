@@ -102,3 +102,35 @@ def test_staged_group_golden(case, monkeypatch):
         g.close()
     y = np.concatenate(res)
     assert sha(y) == case["out_sha256"]
+
+
+@pytest.mark.parametrize("n", [1031, 1000005])
+def test_in_place_host_buffer_p1(ctx, chunk, n):
+    """INTEGRATION.md's shim sorts the reference's own buffer in place:
+    misort_sort_host(ctx, F64, buffer, buffer, ...) with h_in == h_out."""
+    chunk(1 << 14)
+    x = O.generate_f64(n)
+    buf = x.copy()
+    y = ctx.sort_host(buf, out=buf)
+    assert y is buf
+    np.testing.assert_array_equal(buf.view(np.uint64), O.local_sort(x).view(np.uint64))
+
+
+@pytest.mark.parametrize("case", [c for c in PSORT if c["p"] == 8], ids=lambda c: f"N{c['n']}_P8")
+def test_in_place_host_buffer_group(case, monkeypatch):
+    """The same in-place call on every rank of a P = 8 group (exchange stages
+    between the chunked input and the chunked output)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("MISORT_STAGE_CHUNK", str(1 << 14))
+    n, p = case["n"], case["p"]
+    x = O.generate_f64(n)
+    sizes = misort.block_sizes(n, p)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    bufs = [x[offs[r]:offs[r + 1]].copy() for r in range(p)]
+    g = misort.Group(p)
+    try:
+        g.run(lambda r, c: c.sort_host(bufs[r], max_size=n // p + 1, out=bufs[r]))
+    finally:
+        g.close()
+    assert sha(np.concatenate(bufs)) == case["out_sha256"]

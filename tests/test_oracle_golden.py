@@ -111,3 +111,36 @@ def test_defective_layout_is_reproduced():
     # reference; the fixtures hold nonzero error counts and the oracle matches.
     bad = [c for c in GOLD if c["errors"] > 0]
     assert bad and all(c["p"] >= 4 and c.get("algo", "bitonic") == "bitonic" for c in bad)
+
+
+def test_large_fixtures_pinned_by_reference():
+    """tests/golden/large.json: every reference run recorded by
+    make_golden_large.py hashed exactly like the oracle's output."""
+    with open(os.path.join(GOLD_DIR, "large.json")) as f:
+        cases = json.load(f)["cases"]
+    assert {c["config"] for c in cases} == {3, 4, 5}
+    for c in cases:
+        for pin in c.get("pinned_by_reference", []):
+            assert pin["out_sha256"] == c["out_sha256"] and pin["errors"] == c["errors"]
+    assert all(c.get("pinned_by_reference") for c in cases if c["dtype"] == "u32" or c["variant"] == "ref")
+
+
+def test_large_config3_oracle_sha():
+    """The oracle reproduces the reference-pinned 2^28 u32 hash (config 3)."""
+    with open(os.path.join(GOLD_DIR, "large.json")) as f:
+        c = [c for c in json.load(f)["cases"] if c["config"] == 3][0]
+    x = O.splitmix(c["seed"], c["n"], np.uint32)
+    assert hashlib.sha256(x.tobytes()).hexdigest() == c["in_sha256"]
+    y = O.local_sort(x)
+    del x
+    assert hashlib.sha256(y.tobytes()).hexdigest() == c["out_sha256"]
+
+
+def test_u64mix_is_split_invariant_and_mixed():
+    n = 100003
+    x = O.u64mix(0x5EED0005, n)
+    parts = np.concatenate([O.u64mix(0x5EED0005, n, g0=g, cnt=min(7777, n - g)) for g in range(0, n, 7777)])
+    np.testing.assert_array_equal(x, parts)
+    assert 0.03 < np.mean(x == 0) < 0.07 and 0.03 < np.mean(x == np.uint64(O.ALL_ONES)) < 0.07
+    r = O.u64mix(0x5EED0005, n, top=O.REF_TOP)
+    assert r.max() <= np.uint64(O.REF_TOP)
