@@ -245,6 +245,8 @@ def main(argv=None):
         cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
                            args.cpu_sweep, args.cpu_sweep_logn)
 
+    # RCCL logs (its version banner too) go to stderr: stdout is the JSON line
+    os.environ.setdefault("NCCL_DEBUG_FILE", "/dev/stderr")
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -455,7 +457,9 @@ def main(argv=None):
             name, (nl, tms, byt) = dom
             traffic = load_traffic()
             tr = None
-            if traffic and name in traffic and traffic[name].get("bytes_per_launch"):
+            wl = f"{args.dtype}_2e{args.logn}_n{nranks}"
+            if traffic and traffic.get("workload") == wl and name in traffic and \
+                    traffic[name].get("bytes_per_launch"):
                 tr = traffic[name]["bytes_per_launch"]
             achieved = byt / (tms * 1e-3) / 1e9
             out["roofline"] = {"kernel": name, "bound": "hbm", "achieved": achieved,

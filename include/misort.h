@@ -56,8 +56,9 @@ enum misort_kernel_kind {
     MISORT_K_SPAN = 5,        /* tail of one level + head of the next    */
     MISORT_K_WIDE = 6,        /* ROWS strides in a 2^16-key register tile */
     MISORT_K_RUN_MERGE = 7,   /* one merge level: runs 2^hi -> 2^(hi+1)  */
-    MISORT_K_EXCHANGE = 8     /* compare-split exchange leg (splitter samples, RCCL
+    MISORT_K_EXCHANGE = 8,    /* compare-split exchange leg (splitter samples, RCCL
                                  send/recv, codec), device time between events */
+    MISORT_K_RUN_MERGE4 = 9   /* two merge levels in one pass: runs 2^hi -> 2^(hi+2) */
 };
 
 typedef struct misort_ctx misort_ctx;

@@ -78,6 +78,9 @@ struct PlanKnobs {
     // 64 MiB) stay on the network, whose passes are shorter there (2^24:
     // 0.60 vs 0.63 ms, 2^20: 0.18 vs 0.21 ms; 2^28: 10.3 vs 6.8 ms).
     int merge_min_log2_u32 = 24;
+    // u32 merge levels in pairs, one 4-way pass per two levels (runs4.hip);
+    // 0: one 2-way pass per level (MISORT_RUNS4)
+    int runs4 = 1;
     PlanKnobs();
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
@@ -1368,7 +1371,13 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
     const int m0 = kn.merge_from((int)sizeof(K));
     if (runs && m0 > 0 && k > m0 && !(sizeof(K) == 4 && k <= kn.merge_min_log2_u32)) {
         std::vector<Pass> ps = plan_uncached<K, LT, LTR>(m0 < LT ? LT : m0, false);
-        for (int lw = m0 < LT ? LT : m0; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
+        int lw = m0 < LT ? LT : m0;
+        // two levels per pass where the 4-way merge applies (u32); an odd
+        // level left over runs last as a 2-way pass (which keeps host
+        // staging's chunked final pass)
+        if (sizeof(K) == 4 && kn.runs4)
+            for (; lw + 2 <= k && lw >= 15 && lw <= 30; lw += 2) ps.push_back(Pass{KIND_RUNS4, lw, 0, false});
+        for (; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
         return ps;
     }
     const int rmax = kn.rmax < LTR - 5 ? kn.rmax : LTR - 5;
@@ -1415,11 +1424,25 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
     const int np = (int)ps.size();
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
+    int fence_phase = 0;  // 4-way passes: fence buffer holding the next pass's fences
     for (int i = 0; i < np; ++i) {
         // ping-pong: pass i writes `out` iff an even number of passes follow it
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
+        if (p.kind == KIND_RUNS4) {
+            if constexpr (sizeof(K) == 4) {
+                const bool prev4 = i > 0 && ps[i - 1].kind == KIND_RUNS4;
+                const bool next4 = i + 1 < np && ps[i + 1].kind == KIND_RUNS4;
+                const hipError_t e = merge_level4(src, dst, n, p.hi, s, fence_phase, !prev4, next4);
+                if (e != hipSuccess) return e;
+                fence_phase ^= 1;
+                src = dst;
+                continue;
+            } else {
+                return hipErrorInvalidValue;
+            }
+        }
         const bool runs = p.kind == KIND_RUNS;
         const bool contig = p.kind == KIND_TILE_SORT || p.kind == KIND_TILE_MERGE || runs;
         const bool cin = io && io->before_first && i == 0;
@@ -1478,6 +1501,10 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);  // runs of 2^hi -> 2^(hi+1)
+    if (kind == KIND_RUNS4) {  // runs of 2^hi -> 2^(hi+2)
+        if constexpr (sizeof(K) == 4) return merge_level4(in, out, n, hi, s, 0, true, false);
+        return hipErrorInvalidValue;
+    }
     if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER ||
         kind == KIND_EXCHANGE)
         return hipErrorInvalidValue;

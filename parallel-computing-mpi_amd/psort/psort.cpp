@@ -221,13 +221,27 @@ int main(int argc, char** argv) {
             fprintf(stderr, "psort: %d ranks on %d GPU(s): RCCL over sockets (correctness mode)\n", numprocs,
                     ndev);
     }
+    // RCCL logs (its version banner included) go to NCCL_DEBUG_FILE, stdout by
+    // default: keep stdout the reference's six lines
+    setenv("NCCL_DEBUG_FILE", "/dev/stderr", 0);
     misort_ctx* ctx = nullptr;
     misort_ok(misort_create(dev, &ctx), "misort_create");
     if (numprocs > 1) {
+        // RCCL prints its version banner on stdout at init (whatever
+        // NCCL_DEBUG_FILE says): point fd 1 at stderr meanwhile, so stdout
+        // carries the reference's lines only
+        fflush(stdout);
+        const int saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
         unsigned char id[MISORT_UNIQUE_ID_BYTES];
         if (myid == 0) misort_ok(misort_get_unique_id(id), "misort_get_unique_id");
         MPI_Bcast(id, sizeof id, MPI_BYTE, 0, MPI_COMM_WORLD);
         misort_ok(misort_comm_init(ctx, numprocs, myid, id), "misort_comm_init");
+        fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, 1);
+            close(saved);
+        }
     }
 
     std::vector<unsigned char> host((size_t)max_local_size * w + 8);

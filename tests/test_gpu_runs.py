@@ -1,6 +1,7 @@
 """GPU parity of the merge levels (runs.hip) -- the passes that finish the
 local sort replacing the reference's std::sort (psort.cc:175) once runs leave
-the SORT tile.
+the SORT tile: 2-way levels (runs.hip) and 4-way passes of two levels each
+(runs4.hip).
 
 * One merge level (misort_pass_probe, kind run_merge) on inputs made of
   ascending runs of 2^hi keys, ragged tails included, is compared bit for bit
@@ -56,13 +57,21 @@ def expect(x, hi):
     return out
 
 
-def run_level(ctx, x, hi):
+def expect4(x, hi):
+    out = x.copy()
+    w4 = 4 << hi
+    for s in range(0, x.size, w4):
+        out[s:s + w4].sort()
+    return out
+
+
+def run_level(ctx, x, hi, kind="run_merge"):
     if x.dtype == np.uint32:
         d_in = torch.from_numpy(x.view(np.int32)).cuda().view(U32_T)
     else:
         d_in = torch.from_numpy(x.view(np.int64)).cuda().view(U64_T)
     d_out = torch.empty_like(d_in)
-    ctx.pass_probe(d_in, d_out, "run_merge", hi, 0, False, reps=1)
+    ctx.pass_probe(d_in, d_out, kind, hi, 0, False, reps=1)
     torch.cuda.synchronize()
     if x.dtype == np.uint32:
         return d_out.view(torch.int32).cpu().numpy().view(np.uint32)
@@ -87,11 +96,42 @@ def test_merge_level_duplicates_and_single_run(ctx, dt):
         np.testing.assert_array_equal(run_level(ctx, x, hi), expect(x, hi))
 
 
+@pytest.mark.parametrize("hi", [15, 16, 17])
+@pytest.mark.parametrize("n", [(1 << 19), (1 << 19) - 4097, (1 << 18) + 3, 3 * (1 << 17) + 5, 5000, 12345, 2049])
+def test_merge4_level_matches_numpy(ctx, hi, n):
+    """One 4-way pass (runs4.hip): groups of four runs merged, ragged last group
+    (1 to 4 runs, the last one short), fences gathered from the runs."""
+    x = runs_input(n, hi, np.uint32, n + hi)
+    np.testing.assert_array_equal(run_level(ctx, x, hi, "run_merge4"), expect4(x, hi))
+
+
+@pytest.mark.parametrize("hi", [15, 16, 21])
+def test_merge4_level_ties_and_edges(ctx, hi):
+    """Duplicate-heavy, all-equal (every fence the same key: chunks cut by
+    (run, position)), presorted and interleaved runs; hi = 21 merges the
+    fences with two u64 merge levels instead of in LDS."""
+    n = (4 << hi) + (3 << hi) + 1000  # one full group + a 3-run tail
+    cases = [runs_input(n, hi, np.uint32, hi, dup=True), np.full(n, 7, np.uint32),
+             np.arange(n, dtype=np.uint32), np.full(n, 0xFFFFFFFF, np.uint32)]
+    inter = np.arange(n, dtype=np.uint32)  # run r holds r, r+4, r+8, ... of its group
+    w = 1 << hi
+    for g in range(0, n, 4 * w):
+        for r in range(4):
+            seg = inter[g + r * w: g + (r + 1) * w]
+            seg[:] = np.arange(seg.size, dtype=np.uint32) * 4 + r
+    cases.append(inter)
+    for x in cases:
+        np.testing.assert_array_equal(run_level(ctx, x, hi, "run_merge4"), expect4(x, hi))
+
+
 def test_merge_level_rejects_bad_shapes(ctx):
     x = np.arange(1 << 16, dtype=np.uint32)
     for hi in (5, 11):  # runs shorter than the merge tile
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi)
+    for hi in (11, 14):  # 4-way: runs shorter than a chunk
+        with pytest.raises(misort.MisortError):
+            run_level(ctx, x, hi, "run_merge4")
 
 
 CHILD = r"""
@@ -121,7 +161,8 @@ a = out.view(iv).cpu().numpy().view(dt)
 b = d.view(iv).cpu().numpy().view(dt)
 ref = np.sort(keys)
 ok = np.array_equal(a, ref) and np.array_equal(b, ref)
-print("RUNS", sum(1 for p in plan if p[0] == "run_merge"), "OK" if ok else "MISMATCH")
+print("RUNS", sum(1 for p in plan if p[0] == "run_merge") + 2 * sum(1 for p in plan if p[0] == "run_merge4"),
+      "RUNS4", sum(1 for p in plan if p[0] == "run_merge4"), "OK" if ok else "MISMATCH")
 ctx.close()
 """
 
@@ -133,6 +174,10 @@ ctx.close()
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_IT": "32"}, (1 << 21) + 77),
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "256"}, (1 << 21) + 77),
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUNS4": "0"}, (1 << 22) + 4099),
+    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 26) + 12345),  # chained 4-way passes, u64 fence merges
+    (4, {"MISORT_MERGE_FROM": "15"}, 3 * (1 << 23) + 5),
+    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 17) + 1),
     (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),
     (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 21) + 4099),
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_IT": "32"}, (1 << 20) + 5),
@@ -144,8 +189,12 @@ def test_full_sort_merge_from(kb, env, n):
                        text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
-    _, count, verdict = line.split()
+    _, count, _, count4, verdict = line.split()
     assert verdict == "OK", line
+    if kb == 4 and env.get("MISORT_RUNS4") != "0" and int(count) >= 2:
+        assert int(count4) == int(count) // 2  # levels in pairs; an odd one left as a 2-way pass
+    else:
+        assert int(count4) == 0
     m0 = int(next(iter(env.values())))
     if m0 == 0:
         assert int(count) == 0

@@ -15,6 +15,16 @@ import misort
 KIND_SORT, KIND_ROWS, KIND_MERGE, KIND_SPAN = "tile_sort", "global_pass", "tile_merge", "span_pass"
 KIND_WIDE = "wide_pass"  # ROWS stages in the 2^16-key register tile (u32)
 KIND_RUNS = "run_merge"  # one merge level (runs.hip): runs of 2^hi -> 2^(hi+1)
+KIND_RUNS4 = "run_merge4"  # two merge levels in one pass (runs4.hip): runs of 2^hi -> 2^(hi+2)
+MERGES = (KIND_RUNS, KIND_RUNS4)
+
+
+def merge_levels(runs):
+    """Levels (input run log2) the merge passes finish, in order."""
+    out = []
+    for kind, hi, _, _ in runs:
+        out += [hi, hi + 1] if kind == KIND_RUNS4 else [hi]
+    return out
 
 
 def ceil_log2(n):
@@ -28,8 +38,8 @@ def network(k, lt):
 
 def split_runs(plan):
     """(network passes, merge-level passes): merge levels come last."""
-    i = next((j for j, q in enumerate(plan) if q[0] == KIND_RUNS), len(plan))
-    assert all(q[0] == KIND_RUNS for q in plan[i:])
+    i = next((j for j, q in enumerate(plan) if q[0] in MERGES), len(plan))
+    assert all(q[0] in MERGES for q in plan[i:])
     return plan[:i], plan[i:]
 
 
@@ -83,10 +93,12 @@ def replay(keys, plan, lt):
     for m, b in plan_stages(plan, lt):
         stage(x, m, b)
     for kind, hi, _, _ in split_runs(plan)[1]:
-        # merge level: every run of 2^hi is sorted, each pair of runs is merged
+        # merge pass: every run of 2^hi is sorted, each pair (2-way) or group of
+        # four runs (4-way) is merged
         runs = x.reshape(-1, 1 << hi)
         assert np.all(runs[:, 1:] >= runs[:, :-1])
-        x = np.sort(x.reshape(-1, 1 << (hi + 1)), axis=1).reshape(-1)
+        up = 2 if kind == KIND_RUNS4 else 1
+        x = np.sort(x.reshape(-1, 1 << (hi + up)), axis=1).reshape(-1)
     return x[: keys.size]
 
 
@@ -103,7 +115,7 @@ def test_plan_covers_network(n, key_bytes):
     k = ceil_log2(n)
     m0 = merge_from(p, k)
     assert plan_stages(p, lt) == network(min(k, max(m0, lt)), lt)
-    assert [q[1] for q in split_runs(p)[1]] == list(range(m0, k)) if m0 < k else True
+    assert merge_levels(split_runs(p)[1]) == list(range(m0, k)) if m0 < k else True
     for kind, hi, r, flip in p[1:]:
         if kind in (KIND_ROWS, KIND_SPAN):
             assert 1 <= r <= lt - 5  # rows keep >= 32 consecutive keys (128 B for u32)
@@ -112,12 +124,14 @@ def test_plan_covers_network(n, key_bytes):
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + one merge pass per level 16..30 (the network alone
-    # needs 1 + 28 with wide ROWS passes, 1 + 29 without, 1 + 35 level by level)
-    assert len(misort.plan(1 << 30, 4)) == 16
-    assert len(misort.plan(1 << 28, 4)) == 14
+    # 2^30 u32: 1 SORT + seven 4-way passes (levels 16..29 in pairs) + one
+    # 2-way pass for level 30 (one merge pass per level: 1 + 15; the network
+    # alone needs 1 + 28 with wide ROWS passes, 1 + 29 without)
+    assert len(misort.plan(1 << 30, 4)) == 9
+    assert [q[0] for q in misort.plan(1 << 30, 4)] == [KIND_SORT] + [KIND_RUNS4] * 7 + [KIND_RUNS]
+    assert len(misort.plan(1 << 28, 4)) == 8
+    assert [q[0] for q in misort.plan(1 << 29, 4)] == [KIND_SORT] + [KIND_RUNS4] * 7
     assert len(misort.plan(1 << 24, 4)) == 15  # cache-resident u32 sizes stay on the network
-    assert [q[0] for q in misort.plan(1 << 30, 4)] == [KIND_SORT] + [KIND_RUNS] * 15
     # u64: 2^13-key SORT tiles, then merge levels
     assert len(misort.plan((1 << 29) - 3, 8)) == 1 + 29 - 13
 
