@@ -42,12 +42,21 @@ constexpr int FG_LOG2 = 8;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
 constexpr int FM = 31;                          // fences per chunk
 constexpr int CAP = (FM + 4) * (int)FG;         // most keys of a chunk (8960; 7936 on average)
-constexpr int NT = 256;
-constexpr int IT = 36;                          // keys per lane (one merge chain)
-// level 1 puts the second pair's output at the next multiple of IT (no lane
-// straddles two pairs), which needs one spare lane's worth of room
-static_assert(CAP <= (NT - 1) * IT, "chunk tile shape");
-constexpr int LDS_WORDS = NT * IT + IT + 8;
+#ifndef MISORT_M4_NT
+#define MISORT_M4_NT 256
+#endif
+constexpr int NT = MISORT_M4_NT;                // lanes per chunk workgroup
+constexpr int IT = NT == 256 ? 36 : 18;         // keys per lane
+// persistent grid: workgroups per CU the register budget is sized for
+constexpr int WG_PER_CU = NT == 256 ? 4 : 3;
+// Every sequence an in-LDS merge reads is followed by G words of MAX
+// (sentinels), so a merge chain needs no end checks: it reads at most IT words
+// past an exhausted sequence.  Level 1 places the second pair's output at a
+// lane boundary past the first pair's sentinels (no lane straddles two
+// pairs); that layout needs 4 lanes' worth of room beyond CAP.
+constexpr int G = IT + 1;
+static_assert(CAP <= (NT - 4) * IT, "chunk tile shape");
+constexpr int LDS_WORDS = CAP + 4 * G + IT + 16;
 constexpr int DUMP = LDS_WORDS - 1;  // target of masked-off LDS writes (no branches)
 constexpr uint64_t J_MASK = ((uint64_t)1 << 30) - 1;
 
@@ -184,73 +193,78 @@ __global__ void k_bounds4(const uint32_t* __restrict__ src, const uint64_t* __re
     }
 }
 
-// Merge-path co-rank: A keys among the first d outputs of merge(A, B).
+// Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
+// (every A key before it <= every B key after it and vice versa; any such
+// split gives the same output values -- the keys carry no payload).  Fixed
+// 14 halvings (chunks hold < 2^14 keys), no loop control: reads past a
+// sequence land in its sentinels or the word before B0 (in LDS).
 __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d) {
-    int lo = d - LB > 0 ? d - LB : 0, hi = d < LA ? d : LA;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s[A0 + mid] <= s[B0 + d - 1 - mid]) lo = mid + 1;
-        else hi = mid;
+    int base = d - LB > 0 ? d - LB : 0;
+    int len = (d < LA ? d : LA) - base;
+#pragma unroll
+    for (int it = 0; it < 14; ++it) {
+        const int half = len >> 1;
+        const bool right = len > 0 && s[A0 + base + half] <= s[B0 + d - 1 - base - half];
+        base = right ? base + half + 1 : base;
+        len = right ? len - half - 1 : half;
     }
-    return lo;
+    return base;
 }
 
 #ifndef MISORT_M4_CHAINS
-#define MISORT_M4_CHAINS 2
+#define MISORT_M4_CHAINS 1
 #endif
 constexpr int CH = MISORT_M4_CHAINS;  // independent merge chains per lane (interleaved)
 constexpr int IC = IT / CH;
 static_assert(IT % CH == 0, "chains split the lane's outputs");
 
-// IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB))
-// (A first on ties), as CH chains of IC outputs whose dependent LDS reads
-// interleave.  An exhausted side reads as MAX: when it ties a real MAX key of
-// the other side every remaining output is MAX whichever side "wins", so the
-// values stay exact without bounds on the chosen index.  A chain tracks only
-// pa: after step k it has taken d_c + k + 1 keys, so pb = SUM + k - pa.
+// IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
+// both followed by sentinels.  A chain holds h, the head of the side it took
+// last, and g, the other side's head: each step outputs min(h, g), keeps
+// max(h, g) as the other head and reads the next key of the side it took
+// (swapping the two read pointers when that side changes) -- six VALU ops and
+// one LDS read per output.  Ties may go either way: equal keys are identical.
 __device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d,
                                             uint32_t (&r)[IT]) {
     const int tot = LA + LB;
-    const int ea = A0 + LA, eb = B0 + LB;
-    int pa[CH], sum[CH];
-    uint32_t av[CH], bv[CH];
+    int px[CH], py[CH];
+    uint32_t h[CH], g[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int dc = d + c * IC < tot ? d + c * IC : tot;  // lanes past the end: garbage, in-bounds
-        const int lo = co_rank(s, A0, LA, B0, LB, dc);
-        pa[c] = A0 + lo;
-        const int pb = B0 + dc - lo;
-        sum[c] = pa[c] + pb + 1;
-        const uint32_t a0 = s[pa[c]], b0 = s[pb];  // in-bounds: pa <= ea, pb <= eb
-        av[c] = pa[c] < ea ? a0 : 0xFFFFFFFFu;
-        bv[c] = pb < eb ? b0 : 0xFFFFFFFFu;
+        const int ia = co_rank(s, A0, LA, B0, LB, dc);
+        px[c] = A0 + ia;
+        py[c] = B0 + dc - ia;
+        h[c] = s[px[c]];
+        g[c] = s[py[c]];
     }
 #pragma unroll
     for (int k = 0; k < IC; ++k) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            const bool takeA = av[c] <= bv[c];
-            r[c * IC + k] = min(av[c], bv[c]);
-            pa[c] += takeA;
-            const int pb = sum[c] + k - pa[c];
-            const int p = takeA ? pa[c] : pb;
-            const uint32_t v = s[p];
-            const uint32_t w = p < (takeA ? ea : eb) ? v : 0xFFFFFFFFu;
-            av[c] = takeA ? w : av[c];
-            bv[c] = takeA ? bv[c] : w;
+            const bool keep = h[c] <= g[c];
+            r[c * IC + k] = min(h[c], g[c]);
+            const uint32_t o = max(h[c], g[c]);
+            const int nx = keep ? px[c] : py[c];
+            py[c] = keep ? py[c] : px[c];
+            px[c] = nx + 1;
+            h[c] = s[px[c]];
+            g[c] = o;
         }
     }
 }
 
-// MODE (probes only, MISORT_M4_PROBE): 0 = the pass; 1 = loads -> LDS ->
-// stores with no merge (the access pattern's floor); 2 = level 1 only.
-template <bool FENCES, int MODE = 0>
-__global__ __launch_bounds__(NT) void k_merge4(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                               Geo4 geo, const int64_t* __restrict__ bounds,
-                                               uint64_t* __restrict__ fout) {
-    __shared__ __attribute__((aligned(16))) uint32_t s[LDS_WORDS];
-    const int tid = threadIdx.x;
-    const int64_t c = blockIdx.x;
+// Chunk descriptors: for chunk c, the group and the starts/lengths of its four
+// segments (from bounds slots slot(c) and slot(c)+1), validated so that no
+// chunk can address memory outside its group's runs.
+struct Desc {
+    int s[4], l[4];
+    int64_t g;
+};
+
+__global__ void k_chunk_desc(const int64_t* __restrict__ bounds, Geo4 geo, int64_t nchunks, Desc* __restrict__ desc) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
     int64_t g, t;
     if (c < geo.nfull * geo.kf) {
         g = c / geo.kf;
@@ -260,75 +274,133 @@ __global__ __launch_bounds__(NT) void k_merge4(const uint32_t* __restrict__ src,
         t = c - geo.nfull * geo.kf;
     }
     const int64_t* b0 = bounds + 4 * geo.slot(g, t);
-    const int64_t base = geo.base(g);
-    const int64_t W = (int64_t)1 << geo.lw;
-    int s0 = (int)b0[0], s1 = (int)b0[1], s2 = (int)b0[2], s3 = (int)b0[3];
-    int l0 = (int)b0[4] - s0, l1 = (int)b0[5] - s1, l2 = (int)b0[6] - s2, l3 = (int)b0[7] - s3;
+    Desc d;
+    d.g = g;
+    int tot = 0;
+    bool ok = true;
+    for (int r = 0; r < 4; ++r) {
+        const int64_t st = b0[r], ln = b0[4 + r] - st;
+        ok = ok && st >= 0 && ln >= 0 && st + ln <= geo.run_len(g, r);
+        d.s[r] = (int)st;
+        d.l[r] = (int)ln;
+        tot += ok ? (int)ln : 0;
+    }
     // bounds outside the runs would be a logic error: never let them address
     // memory (the chunk is then left unwritten and the sort fails its checks)
-    if (s0 < 0 || l0 < 0 || s0 + l0 > geo.run_len(g, 0) || s1 < 0 || l1 < 0 || s1 + l1 > geo.run_len(g, 1) ||
-        s2 < 0 || l2 < 0 || s2 + l2 > geo.run_len(g, 2) || s3 < 0 || l3 < 0 || s3 + l3 > geo.run_len(g, 3) ||
-        l0 + l1 + l2 + l3 > CAP)
-        s0 = s1 = s2 = s3 = l0 = l1 = l2 = l3 = 0;
-    const int o1 = l0, o2 = o1 + l1, o3 = o2 + l2;
-    const int len = o3 + l3 < CAP ? o3 + l3 : CAP;  // <= CAP by construction; never past the LDS tile
-    const int64_t out0 = base + s0 + s1 + s2 + s3;
-    // segment r occupies chunk positions [o_r, o_r + l_r); its key at chunk
-    // position e is gsrc[d_r + e] (32-bit offsets within the group: 4W <= 2^32;
-    // d_r >= 0 as W >= CAP)
-    const uint32_t* __restrict__ gsrc = src + base;
-    const uint32_t dA = (uint32_t)s0, dB = (uint32_t)W + s1 - o1, dC = 2u * (uint32_t)W + s2 - o2,
-                   dD = 3u * (uint32_t)W + s3 - o3;
-    {
-        uint32_t x[IT];
+    if (!ok || tot > CAP)
+        for (int r = 0; r < 4; ++r) d.s[r] = d.l[r] = 0;
+    desc[c] = d;
+}
+
+// One chunk's place: its four segments (chunk positions [o_r, o_r + l_r),
+// key at chunk position e = gsrc[d_r + e]) and its output offset.
+struct Chunk {
+    const uint32_t* gsrc;
+    uint32_t dA, dB, dC, dD;
+    int o1, o2, o3, len, l0, l2;
+    int64_t out0;
+};
+
+__device__ __forceinline__ Chunk chunk_of(const uint32_t* src, const Geo4& geo, const Desc* desc, int64_t c) {
+    const Desc& dc = desc[c];
+    const int64_t g = dc.g;
+    const int64_t base = geo.base(g);
+    const int64_t W = (int64_t)1 << geo.lw;
+    const int s0 = dc.s[0], s1 = dc.s[1], s2 = dc.s[2], s3 = dc.s[3];
+    const int l0 = dc.l[0], l1 = dc.l[1], l2 = dc.l[2], l3 = dc.l[3];
+    Chunk k;
+    k.o1 = l0;
+    k.o2 = k.o1 + l1;
+    k.o3 = k.o2 + l2;
+    k.len = k.o3 + l3;  // <= CAP by construction and the check above
+    k.l0 = l0;
+    k.l2 = l2;
+    k.out0 = base + s0 + s1 + s2 + s3;
+    // 32-bit offsets within the group (4W <= 2^32; d_r >= 0 as W >= CAP)
+    k.gsrc = src + base;
+    k.dA = (uint32_t)s0;
+    k.dB = (uint32_t)W + s1 - k.o1;
+    k.dC = 2u * (uint32_t)W + s2 - k.o2;
+    k.dD = 3u * (uint32_t)W + s3 - k.o3;
+    return k;
+}
+
+__device__ __forceinline__ void chunk_loads(const Chunk& k, int tid, uint32_t (&x)[IT]) {
 #pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const int e = k * NT + tid;
-            const uint32_t d = e < o1 ? dA : e < o2 ? dB : e < o3 ? dC : dD;
-            x[k] = e < len ? __builtin_nontemporal_load(gsrc + (d + (uint32_t)e)) : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int k = 0; k < IT; ++k) s[k * NT + tid] = x[k];
+    for (int j = 0; j < IT; ++j) {
+        const int e = j * NT + tid;
+        const uint32_t d = e < k.o1 ? k.dA : e < k.o2 ? k.dB : e < k.o3 ? k.dC : k.dD;
+        x[j] = e < k.len ? __builtin_nontemporal_load(k.gsrc + (d + (uint32_t)e)) : 0xFFFFFFFFu;
     }
-    __syncthreads();
+}
+
+// Chunk position e of segment r goes to LDS word e + r*G, so G sentinel words
+// follow every segment.
+__device__ __forceinline__ void chunk_to_lds(uint32_t* s, const Chunk& k, int tid, const uint32_t (&x)[IT]) {
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const int e = j * NT + tid;
+        const int w = e + (e < k.o1 ? 0 : e < k.o2 ? G : e < k.o3 ? 2 * G : 3 * G);
+        s[e < k.len ? w : DUMP] = x[j];
+    }
+    if (tid < 4 * G) {  // the sentinels after segments 0..3
+        const int r = tid / G, i = tid - r * G;
+        const int end = r == 0 ? k.o1 : r == 1 ? k.o2 : r == 2 ? k.o3 : k.len;
+        s[end + r * G + i] = 0xFFFFFFFFu;
+    }
+}
+
+// The two in-LDS merge levels of a chunk, its stores and fences.  MODE
+// (probes only, MISORT_M4_PROBE): 0 = the pass; 1 = no merge (the access
+// pattern's floor); 2 = level 1 only.
+template <bool FENCES, int MODE>
+__device__ __forceinline__ void chunk_merge(uint32_t* s, const Chunk& k, int tid, uint32_t* __restrict__ dst,
+                                            uint64_t* __restrict__ fout, int lwn) {
+    const int o1 = k.o1, o2 = k.o2, o3 = k.o3, len = k.len;
+    const int l0 = k.l0, l1 = o2 - o1, l2 = k.l2, l3 = len - o3;
     uint32_t r[IT];
     const int pos = tid * IT;
-    // level 1: A ++ B -> [0, o2); C ++ D -> [q2, q2 + l2 + l3), q2 = o2 rounded
-    // up to a lane boundary, so each lane merges inside one pair
-    const int q2 = (o2 + IT - 1) / IT * IT, end1 = q2 + (len - o2);
+    // level 1: segments at e + r*G (chunk_to_lds).  A ++ B -> [0, o2) and
+    // C ++ D -> [q2, q2 + l2 + l3), q2 = the first lane boundary past A ++ B's
+    // sentinels [o2, o2 + G); sentinels follow C ++ D too
+    const int q2 = (o2 + G + IT - 1) / IT * IT, end1 = q2 + (len - o2);
     const bool p1 = pos < o2;
     if constexpr (MODE == 1) {
 #pragma unroll
-        for (int k = 0; k < IT; ++k) r[k] = s[pos + k];
+        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < DUMP ? pos + j : DUMP];
     } else {
-        merge_chain(s, p1 ? 0 : o2, p1 ? l0 : l2, p1 ? o1 : o3, p1 ? l1 : l3, p1 ? pos : pos - q2, r);
+        merge_chain(s, p1 ? 0 : o2 + 2 * G, p1 ? l0 : l2, p1 ? o1 + G : o3 + 3 * G, p1 ? l1 : l3,
+                    p1 ? pos : pos - q2, r);
     }
     __syncthreads();
     {
         const int lim = p1 ? o2 : end1;
-        if (pos + IT <= lim) {
+        const bool act = p1 || pos >= q2;
+        if (act && pos + IT <= lim) {
             typedef uint32_t vec2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-            for (int k = 0; k < IT; k += 2) *reinterpret_cast<vec2*>(s + pos + k) = vec2{r[k], r[k + 1]};
+            for (int j = 0; j < IT; j += 2) *reinterpret_cast<vec2*>(s + pos + j) = vec2{r[j], r[j + 1]};
         } else {
 #pragma unroll
-            for (int k = 0; k < IT; ++k) s[pos + k < lim ? pos + k : DUMP] = r[k];
+            for (int j = 0; j < IT; ++j) s[act && pos + j < lim ? pos + j : DUMP] = r[j];
         }
+        if (tid < 2 * G) s[tid < G ? o2 + tid : end1 + tid - G] = 0xFFFFFFFFu;
     }
     __syncthreads();
     // level 2: [0, o2) ++ [q2, end1) -> the chunk
     if constexpr (MODE != 0) {
 #pragma unroll
-        for (int k = 0; k < IT; ++k) r[k] = s[pos + k];
+        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < DUMP ? pos + j : DUMP];
     } else {
         merge_chain(s, 0, o2, q2, len - o2, pos, r);
     }
     __syncthreads();
     // the chunk goes to LDS shifted by out0 mod 4, so every global 16-byte
     // vector is one aligned LDS vector
+    const int64_t out0 = k.out0;
     const int sh = (int)(out0 & 3);
 #pragma unroll
-    for (int k = 0; k < IT; ++k) s[pos + k < len ? sh + pos + k : DUMP] = r[k];
+    for (int j = 0; j < IT; ++j) s[pos + j < len ? sh + pos + j : DUMP] = r[j];
     __syncthreads();
     const int nv = (sh + len + 3) >> 2;
     uint32_t* __restrict__ o = dst + (out0 - sh);
@@ -349,8 +421,45 @@ __global__ __launch_bounds__(NT) void k_merge4(const uint32_t* __restrict__ src,
         const int nf = first < out0 + len ? (int)((out0 + len - first + FG - 1) >> FG_LOG2) : 0;
         if (tid < nf) {
             const int64_t gp = first + ((int64_t)tid << FG_LOG2);
-            fout[gp >> FG_LOG2] = fpack(s[(int)(gp - (out0 - sh))], gp, geo.lw + 2);
+            fout[gp >> FG_LOG2] = fpack(s[(int)(gp - (out0 - sh))], gp, lwn);
         }
+    }
+}
+
+// Persistent workgroups walk the chunks; the next chunk's 36 loads per lane
+// are in flight (registers) while the current chunk merges, so the HBM
+// stream does not stop during the LDS phases.
+template <bool FENCES, int MODE = 0>
+__global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_merge4(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                               Geo4 geo, const Desc* __restrict__ desc,
+                                               uint64_t* __restrict__ fout, int64_t nchunks) {
+    __shared__ __attribute__((aligned(16))) uint32_t s[LDS_WORDS];
+    const int tid = threadIdx.x;
+    int64_t c = blockIdx.x;
+    if (c >= nchunks) return;
+    Chunk k = chunk_of(src, geo, desc, c);
+    uint32_t x[IT];
+    chunk_loads(k, tid, x);
+    for (;;) {
+        // lane id through an opaque copy: lane-derived addresses are recomputed
+        // every chunk instead of being hoisted into loop-invariant VGPRs, which
+        // spilled -- and a spill reload waits (in-order vmcnt) for the whole
+        // prefetch issued before it
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        chunk_to_lds(s, k, t, x);
+        __syncthreads();
+        const int64_t cn = c + gridDim.x;
+        Chunk kn = k;
+        if (cn < nchunks) {
+            kn = chunk_of(src, geo, desc, cn);
+            chunk_loads(kn, t, x);
+        }
+        chunk_merge<FENCES, MODE>(s, k, t, dst, fout, geo.lw + 2);
+        if (cn >= nchunks) break;
+        __syncthreads();  // the next chunk overwrites the tile
+        c = cn;
+        k = kn;
     }
 }
 
@@ -404,13 +513,15 @@ hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, h
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
     // layout: fence buffers 0 and 1, merged fences, u64 merge temp, bounds
     const size_t fb = ((size_t)nf * 8 + 255) & ~(size_t)255;
-    char* base = (char*)scratch4(4 * fb + (size_t)nslots * 32 + 256, s);
+    const size_t bb = ((size_t)nslots * 32 + 255) & ~(size_t)255;
+    char* base = (char*)scratch4(4 * fb + bb + (size_t)nchunks * sizeof(Desc) + 256, s);
     if (!base) return hipErrorOutOfMemory;
     uint64_t* F = (uint64_t*)(base + (phase & 1) * fb);
     uint64_t* Fn = (uint64_t*)(base + ((phase & 1) ^ 1) * fb);
     uint64_t* M = (uint64_t*)(base + 2 * fb);
     uint64_t* T = (uint64_t*)(base + 3 * fb);
     int64_t* bounds = (int64_t*)(base + 4 * fb);
+    Desc* desc = (Desc*)(base + 4 * fb + bb);
     if (gather) k_fence_gather<<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, F);
     const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
     if (wf_log2 <= 11) {  // group fences <= 8192: 64 KiB of LDS
@@ -423,8 +534,18 @@ hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, h
         if (e != hipSuccess) return e;
     }
     k_bounds4<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(src, F, M, geo, nslots, bounds);
-    if (write_next) k_merge4<true><<<(unsigned)nchunks, NT, 0, s>>>(src, dst, geo, bounds, Fn);
-    else k_merge4<false><<<(unsigned)nchunks, NT, 0, s>>>(src, dst, geo, bounds, nullptr);
+    k_chunk_desc<<<(unsigned)((nchunks + 255) / 256), 256, 0, s>>>(bounds, geo, nchunks, desc);
+    static int64_t cap = 0;  // resident workgroups (the persistent grid)
+    if (cap == 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_merge4<true>, NT, 0);
+        cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
+    }
+    const unsigned grid = (unsigned)(nchunks < cap ? nchunks : cap);
+    if (write_next) k_merge4<true><<<grid, NT, 0, s>>>(src, dst, geo, desc, Fn, nchunks);
+    else k_merge4<false><<<grid, NT, 0, s>>>(src, dst, geo, desc, nullptr, nchunks);
     static const bool probe = getenv("MISORT_M4_PROBE") && atoi(getenv("MISORT_M4_PROBE")) != 0;
     if (probe) {
         // same chunks and bounds, outputs to a scratch buffer (the sort is untouched)
@@ -436,8 +557,8 @@ hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, h
             if (hipMalloc(&junk, (size_t)n * 4) != hipSuccess) return hipErrorOutOfMemory;
             junk_n = (size_t)n;
         }
-        k_merge4<false, 1><<<(unsigned)nchunks, NT, 0, s>>>(src, junk, geo, bounds, nullptr);
-        k_merge4<false, 2><<<(unsigned)nchunks, NT, 0, s>>>(src, junk, geo, bounds, nullptr);
+        k_merge4<false, 1><<<grid, NT, 0, s>>>(src, junk, geo, desc, nullptr, nchunks);
+        k_merge4<false, 2><<<grid, NT, 0, s>>>(src, junk, geo, desc, nullptr, nchunks);
     }
     return hipGetLastError();
 }
