@@ -1376,7 +1376,7 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
         // level left over runs last as a 2-way pass (which keeps host
         // staging's chunked final pass)
         if (sizeof(K) == 4 && kn.runs4)
-            for (; lw + 2 <= k && lw >= 15 && lw <= 30; lw += 2) ps.push_back(Pass{KIND_RUNS4, lw, 0, false});
+            for (; lw + 2 <= k && lw >= 15 && lw <= 28; lw += 2) ps.push_back(Pass{KIND_RUNS4, lw, 0, false});
         for (; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
         return ps;
     }

@@ -40,27 +40,39 @@ namespace {
 
 constexpr int FG_LOG2 = 8;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
-constexpr int FM = 31;                          // fences per chunk
-constexpr int CAP = (FM + 4) * (int)FG;         // most keys of a chunk (8960; 7936 on average)
+constexpr int FM = 28;                          // fences per chunk
+constexpr int CAP = (FM + 4) * (int)FG;         // most keys of a chunk (8192; 7168 on average)
 #ifndef MISORT_M4_NT
-#define MISORT_M4_NT 256
+#define MISORT_M4_NT 512
 #endif
 constexpr int NT = MISORT_M4_NT;                // lanes per chunk workgroup
 constexpr int IT = NT == 256 ? 36 : 18;         // keys per lane
-// persistent grid: workgroups per CU the register budget is sized for
-constexpr int WG_PER_CU = NT == 256 ? 4 : 3;
+// persistent grid: workgroups per CU the register budget is sized for (the
+// LDS tile allows 4)
+constexpr int WG_PER_CU = 4;
+// load rows: RW consecutive keys of one segment; a lane's load slot j holds
+// row j * (NT / RW) + tid / RW -- one row per wave and slot
+constexpr int RW = 256;
+constexpr int NROWS = IT * NT / RW;
 // Every sequence an in-LDS merge reads is followed by G words of MAX
 // (sentinels), so a merge chain needs no end checks: it reads at most IT words
 // past an exhausted sequence.  Level 1 places the second pair's output at a
 // lane boundary past the first pair's sentinels (no lane straddles two
-// pairs); that layout needs 4 lanes' worth of room beyond CAP.
+// pairs); that layout needs 4 lanes' worth of room beyond CAP.  A chunk is
+// loaded in rows of NT keys, each row within one segment, so the four
+// segments take at most CAP/NT + 4 rows of the lanes' IT load slots.
 constexpr int G = IT + 1;
-static_assert(CAP <= (NT - 4) * IT, "chunk tile shape");
-constexpr int LDS_WORDS = CAP + 4 * G + IT + 16;
-constexpr int DUMP = LDS_WORDS - 1;  // target of masked-off LDS writes (no branches)
+static_assert(CAP <= (NT - 4) * IT, "chunk tile shape (level-1 layout)");
+static_assert(CAP <= (NROWS - 4) * RW, "chunk tile shape (segment rows)");
+constexpr int PAD = 4;  // words below the tile: a co-rank probe may read index -1
+constexpr int LDS_WORDS = PAD + CAP + 4 * G + 2 * IT + 16;
 constexpr uint64_t J_MASK = ((uint64_t)1 << 30) - 1;
 
 typedef uint32_t vec4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return (uint32_t)(uintptr_t)(const lds_u32*)p; }
+__device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(const lds_u32*)(uintptr_t)a; }
 
 __device__ __forceinline__ uint64_t fpack(uint32_t key, int64_t gp, int lw) {
     const uint64_t r = (uint64_t)(gp >> lw) & 3;
@@ -195,28 +207,27 @@ __global__ void k_bounds4(const uint32_t* __restrict__ src, const uint64_t* __re
 
 // Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
 // (every A key before it <= every B key after it and vice versa; any such
-// split gives the same output values -- the keys carry no payload).  Fixed
-// 14 halvings (chunks hold < 2^14 keys), no loop control: reads past a
-// sequence land in its sentinels or the word before B0 (in LDS).
+// split gives the same output values -- the keys carry no payload).  The
+// largest base in [lo, hi] with A[i - 1] <= B[d - i] for every i <= base, by
+// 13 power-of-two steps (hi - lo <= min(LA, LB) <= CAP/2 = 2^12) with clamped
+// probes: no loop control, no branches.  Probe addresses stay inside
+// [A0 - 1, A0 + LA) and [B0, B0 + LB].
 __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d) {
-    int base = d - LB > 0 ? d - LB : 0;
-    int len = (d < LA ? d : LA) - base;
+    static_assert(CAP / 2 <= 4096 * 2 - 1, "co-rank steps");
+    const int lo = d - LB > 0 ? d - LB : 0;
+    const int hi = d < LA ? d : LA;
+    const uint32_t* a = s + A0 - 1;
+    const uint32_t* b = s + B0 + d;
+    int base = lo;
 #pragma unroll
-    for (int it = 0; it < 14; ++it) {
-        const int half = len >> 1;
-        const bool right = len > 0 && s[A0 + base + half] <= s[B0 + d - 1 - base - half];
-        base = right ? base + half + 1 : base;
-        len = right ? len - half - 1 : half;
+    for (int step = 4096; step >= 1; step >>= 1) {
+        const int i = base + step;
+        const int ic = i < hi ? i : hi;
+        const bool ok = i <= hi && a[ic] <= b[-ic];
+        base = ok ? i : base;
     }
     return base;
 }
-
-#ifndef MISORT_M4_CHAINS
-#define MISORT_M4_CHAINS 1
-#endif
-constexpr int CH = MISORT_M4_CHAINS;  // independent merge chains per lane (interleaved)
-constexpr int IC = IT / CH;
-static_assert(IT % CH == 0, "chains split the lane's outputs");
 
 // IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
 // both followed by sentinels.  A chain holds h, the head of the side it took
@@ -224,47 +235,52 @@ static_assert(IT % CH == 0, "chains split the lane's outputs");
 // max(h, g) as the other head and reads the next key of the side it took
 // (swapping the two read pointers when that side changes) -- six VALU ops and
 // one LDS read per output.  Ties may go either way: equal keys are identical.
+// Past the end of both sequences a chain outputs MAX (their sentinels).
 __device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d,
                                             uint32_t (&r)[IT]) {
     const int tot = LA + LB;
-    int px[CH], py[CH];
-    uint32_t h[CH], g[CH];
+    const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
+    const int ia = co_rank(s, A0, LA, B0, LB, dc);
+    // byte addresses of the two heads (LDS pointers are 32-bit)
+    uint32_t px = lds_addr(s + A0 + ia), py = lds_addr(s + B0 + dc - ia);
+    uint32_t h = lds_ld(px), g = lds_ld(py);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int dc = d + c * IC < tot ? d + c * IC : tot;  // lanes past the end: garbage, in-bounds
-        const int ia = co_rank(s, A0, LA, B0, LB, dc);
-        px[c] = A0 + ia;
-        py[c] = B0 + dc - ia;
-        h[c] = s[px[c]];
-        g[c] = s[py[c]];
-    }
-#pragma unroll
-    for (int k = 0; k < IC; ++k) {
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const bool keep = h[c] <= g[c];
-            r[c * IC + k] = min(h[c], g[c]);
-            const uint32_t o = max(h[c], g[c]);
-            const int nx = keep ? px[c] : py[c];
-            py[c] = keep ? py[c] : px[c];
-            px[c] = nx + 1;
-            h[c] = s[px[c]];
-            g[c] = o;
-        }
+    for (int k = 0; k < IT; ++k) {
+        const bool keep = h <= g;
+        r[k] = min(h, g);
+        const uint32_t o = max(h, g);
+        const uint32_t nx = keep ? px : py;
+        py = keep ? py : px;
+        px = nx + 4;
+        h = lds_ld(px);
+        g = o;
     }
 }
 
-// Chunk descriptors: for chunk c, the group and the starts/lengths of its four
-// segments (from bounds slots slot(c) and slot(c)+1), validated so that no
-// chunk can address memory outside its group's runs.
+// Chunk descriptors: for chunk c, its group's base, its output offset, the
+// chunk positions where its four segments start, and its LOAD ROWS.  A chunk
+// is loaded in NROWS rows of RW consecutive keys, each row inside one segment
+// (segment r takes ceil(l_r / RW) rows; the four take <= CAP/RW + 4 = NROWS):
+// row j = byte offset of its first key from the group base, and how many of
+// its NT keys are real plus the LDS word the first goes to (segment r's keys
+// start at LDS word o_r + r*G, leaving G words for sentinels after each).
+// Validated so that no chunk can address memory outside its group's runs:
+// a bad chunk gets no rows and is left unwritten (the sort then fails its
+// checks).
 struct Desc {
-    int s[4], l[4];
-    int64_t g;
+    int64_t gbase, out0;
+    int o1, o2, o3, len;
+    uint32_t off[NROWS];  // row j: byte offset of its first key from the group base
+    uint32_t la[NROWS];   // row j: real keys (0..RW) | LDS word of its first key << 16
 };
+static_assert(CAP + 4 * (IT + 1) < 65536, "LDS word fits 16 bits");
 
+// One thread per (chunk, row); row slot NROWS writes the header.
 __global__ void k_chunk_desc(const int64_t* __restrict__ bounds, Geo4 geo, int64_t nchunks, Desc* __restrict__ desc) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nchunks * (NROWS + 1)) return;
+    const int64_t c = id / (NROWS + 1);
+    const int j = (int)(id - c * (NROWS + 1));
     int64_t g, t;
     if (c < geo.nfull * geo.kf) {
         g = c / geo.kf;
@@ -274,133 +290,129 @@ __global__ void k_chunk_desc(const int64_t* __restrict__ bounds, Geo4 geo, int64
         t = c - geo.nfull * geo.kf;
     }
     const int64_t* b0 = bounds + 4 * geo.slot(g, t);
-    Desc d;
-    d.g = g;
-    int tot = 0;
+    int64_t st[4], ln[4], tot = 0;
     bool ok = true;
     for (int r = 0; r < 4; ++r) {
-        const int64_t st = b0[r], ln = b0[4 + r] - st;
-        ok = ok && st >= 0 && ln >= 0 && st + ln <= geo.run_len(g, r);
-        d.s[r] = (int)st;
-        d.l[r] = (int)ln;
-        tot += ok ? (int)ln : 0;
+        st[r] = b0[r];
+        ln[r] = b0[4 + r] - st[r];
+        ok = ok && st[r] >= 0 && ln[r] >= 0 && st[r] + ln[r] <= geo.run_len(g, r);
+        tot += ok ? ln[r] : 0;
     }
-    // bounds outside the runs would be a logic error: never let them address
-    // memory (the chunk is then left unwritten and the sort fails its checks)
-    if (!ok || tot > CAP)
-        for (int r = 0; r < 4; ++r) d.s[r] = d.l[r] = 0;
-    desc[c] = d;
+    ok = ok && tot <= CAP;
+    // bounds outside the runs would be a logic error: never let them address memory
+    if (!ok)
+        for (int r = 0; r < 4; ++r) st[r] = ln[r] = 0;
+    Desc& d = desc[c];
+    if (j == NROWS) {
+        d.gbase = geo.base(g);
+        d.out0 = geo.base(g) + st[0] + st[1] + st[2] + st[3];
+        d.o1 = (int)ln[0];
+        d.o2 = (int)(ln[0] + ln[1]);
+        d.o3 = (int)(ln[0] + ln[1] + ln[2]);
+        d.len = (int)(ln[0] + ln[1] + ln[2] + ln[3]);
+        return;
+    }
+    int R = 0, o = 0;
+    uint32_t off = 0, la = 0;
+    for (int r = 0; r < 4; ++r) {
+        const int rows = (int)((ln[r] + RW - 1) / RW);
+        if (j >= R && j < R + rows) {
+            const int k = j - R;
+            const int64_t rem = ln[r] - (int64_t)k * RW;
+            off = (uint32_t)((((int64_t)r << geo.lw) + st[r] + (int64_t)k * RW) * 4);  // < 4W*4 <= 2^32 (lw <= 28)
+            la = (uint32_t)(rem < RW ? rem : RW) | ((uint32_t)(o + r * G + k * RW) << 16);
+        }
+        R += rows;
+        o += (int)ln[r];
+    }
+    d.off[j] = off;
+    d.la[j] = la;  // rows past the chunk: no keys
 }
 
-// One chunk's place: its four segments (chunk positions [o_r, o_r + l_r),
-// key at chunk position e = gsrc[d_r + e]) and its output offset.
-struct Chunk {
-    const uint32_t* gsrc;
-    uint32_t dA, dB, dC, dD;
-    int o1, o2, o3, len, l0, l2;
-    int64_t out0;
-};
+// The wave's row half (uniform) and the lane's place in its row.
+__device__ __forceinline__ int row_half(int tid) { return __builtin_amdgcn_readfirstlane(tid) / RW; }
 
-__device__ __forceinline__ Chunk chunk_of(const uint32_t* src, const Geo4& geo, const Desc* desc, int64_t c) {
-    const Desc& dc = desc[c];
-    const int64_t g = dc.g;
-    const int64_t base = geo.base(g);
-    const int64_t W = (int64_t)1 << geo.lw;
-    const int s0 = dc.s[0], s1 = dc.s[1], s2 = dc.s[2], s3 = dc.s[3];
-    const int l0 = dc.l[0], l1 = dc.l[1], l2 = dc.l[2], l3 = dc.l[3];
-    Chunk k;
-    k.o1 = l0;
-    k.o2 = k.o1 + l1;
-    k.o3 = k.o2 + l2;
-    k.len = k.o3 + l3;  // <= CAP by construction and the check above
-    k.l0 = l0;
-    k.l2 = l2;
-    k.out0 = base + s0 + s1 + s2 + s3;
-    // 32-bit offsets within the group (4W <= 2^32; d_r >= 0 as W >= CAP)
-    k.gsrc = src + base;
-    k.dA = (uint32_t)s0;
-    k.dB = (uint32_t)W + s1 - k.o1;
-    k.dC = 2u * (uint32_t)W + s2 - k.o2;
-    k.dD = 3u * (uint32_t)W + s3 - k.o3;
-    return k;
-}
-
-__device__ __forceinline__ void chunk_loads(const Chunk& k, int tid, uint32_t (&x)[IT]) {
+__device__ __forceinline__ void chunk_loads(const uint32_t* src, const Desc* d, int tid, uint32_t (&x)[IT]) {
+    const char* gsrc = (const char*)(src + d->gbase);
+    const int h = row_half(tid), lt = tid & (RW - 1);
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-        const int e = j * NT + tid;
-        const uint32_t d = e < k.o1 ? k.dA : e < k.o2 ? k.dB : e < k.o3 ? k.dC : k.dD;
-        x[j] = e < k.len ? __builtin_nontemporal_load(k.gsrc + (d + (uint32_t)e)) : 0xFFFFFFFFu;
+        const int row = j * (NT / RW) + h;
+        const int lim = (int)(d->la[row] & 0xFFFF);
+        if (lt < lim) x[j] = __builtin_nontemporal_load((const uint32_t*)(gsrc + d->off[row]) + (uint32_t)lt);
     }
 }
 
-// Chunk position e of segment r goes to LDS word e + r*G, so G sentinel words
-// follow every segment.
-__device__ __forceinline__ void chunk_to_lds(uint32_t* s, const Chunk& k, int tid, const uint32_t (&x)[IT]) {
+// Row j's real keys go to their LDS words; then the G sentinel words after
+// every segment.
+__device__ __forceinline__ void chunk_to_lds(uint32_t* s, const Desc* d, int tid, const uint32_t (&x)[IT]) {
+    const int h = row_half(tid), lt = tid & (RW - 1);
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
-        const int e = j * NT + tid;
-        const int w = e + (e < k.o1 ? 0 : e < k.o2 ? G : e < k.o3 ? 2 * G : 3 * G);
-        s[e < k.len ? w : DUMP] = x[j];
+        const uint32_t la = d->la[j * (NT / RW) + h];
+        if (lt < (int)(la & 0xFFFF)) s[(la >> 16) + lt] = x[j];
     }
-    if (tid < 4 * G) {  // the sentinels after segments 0..3
+    if (tid < 4 * G) {
         const int r = tid / G, i = tid - r * G;
-        const int end = r == 0 ? k.o1 : r == 1 ? k.o2 : r == 2 ? k.o3 : k.len;
+        const int end = r == 0 ? d->o1 : r == 1 ? d->o2 : r == 2 ? d->o3 : d->len;
         s[end + r * G + i] = 0xFFFFFFFFu;
     }
 }
 
 // The two in-LDS merge levels of a chunk, its stores and fences.  MODE
 // (probes only, MISORT_M4_PROBE): 0 = the pass; 1 = no merge (the access
-// pattern's floor); 2 = level 1 only.
+// pattern's floor); 2 = level 1 only.  Waves whose lanes all lie past a
+// level's outputs skip its merge (a chunk averages 7168 of 9216 lane slots).
 template <bool FENCES, int MODE>
-__device__ __forceinline__ void chunk_merge(uint32_t* s, const Chunk& k, int tid, uint32_t* __restrict__ dst,
+__device__ __forceinline__ void chunk_merge(uint32_t* s, const Desc* dc, int tid, uint32_t* __restrict__ dst,
                                             uint64_t* __restrict__ fout, int lwn) {
-    const int o1 = k.o1, o2 = k.o2, o3 = k.o3, len = k.len;
-    const int l0 = k.l0, l1 = o2 - o1, l2 = k.l2, l3 = len - o3;
+    const int o1 = dc->o1, o2 = dc->o2, o3 = dc->o3, len = dc->len;
+    const int l0 = o1, l1 = o2 - o1, l2 = o3 - o2, l3 = len - o3;
+    constexpr int LAST = LDS_WORDS - PAD - 1;
     uint32_t r[IT];
     const int pos = tid * IT;
+    const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
     // level 1: segments at e + r*G (chunk_to_lds).  A ++ B -> [0, o2) and
     // C ++ D -> [q2, q2 + l2 + l3), q2 = the first lane boundary past A ++ B's
     // sentinels [o2, o2 + G); sentinels follow C ++ D too
     const int q2 = (o2 + G + IT - 1) / IT * IT, end1 = q2 + (len - o2);
     const bool p1 = pos < o2;
+    const bool act = p1 || (pos >= q2 && pos < end1);
     if constexpr (MODE == 1) {
 #pragma unroll
-        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < DUMP ? pos + j : DUMP];
-    } else {
-        merge_chain(s, p1 ? 0 : o2 + 2 * G, p1 ? l0 : l2, p1 ? o1 + G : o3 + 3 * G, p1 ? l1 : l3,
-                    p1 ? pos : pos - q2, r);
+        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
+    } else if (wpos < end1) {
+        const int d = p1 ? pos : (pos > q2 ? pos - q2 : 0);
+        merge_chain(s, p1 ? 0 : o2 + 2 * G, p1 ? l0 : l2, p1 ? o1 + G : o3 + 3 * G, p1 ? l1 : l3, d, r);
     }
     __syncthreads();
-    {
-        const int lim = p1 ? o2 : end1;
-        const bool act = p1 || pos >= q2;
-        if (act && pos + IT <= lim) {
-            typedef uint32_t vec2 __attribute__((ext_vector_type(2)));
+    // a lane's outputs past its pair's end are MAX (the chain ran into the
+    // sentinels), the same value the sentinel stores write there
+    if (act) {
+        typedef uint32_t vec2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-            for (int j = 0; j < IT; j += 2) *reinterpret_cast<vec2*>(s + pos + j) = vec2{r[j], r[j + 1]};
-        } else {
-#pragma unroll
-            for (int j = 0; j < IT; ++j) s[act && pos + j < lim ? pos + j : DUMP] = r[j];
-        }
-        if (tid < 2 * G) s[tid < G ? o2 + tid : end1 + tid - G] = 0xFFFFFFFFu;
+        for (int j = 0; j < IT; j += 2) *reinterpret_cast<vec2*>(s + pos + j) = vec2{r[j], r[j + 1]};
     }
+    if (tid < 2 * G) s[tid < G ? o2 + tid : end1 + tid - G] = 0xFFFFFFFFu;
     __syncthreads();
     // level 2: [0, o2) ++ [q2, end1) -> the chunk
     if constexpr (MODE != 0) {
 #pragma unroll
-        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < DUMP ? pos + j : DUMP];
-    } else {
+        for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
+    } else if (wpos < len) {
         merge_chain(s, 0, o2, q2, len - o2, pos, r);
     }
     __syncthreads();
     // the chunk goes to LDS shifted by out0 mod 4, so every global 16-byte
-    // vector is one aligned LDS vector
-    const int64_t out0 = k.out0;
+    // vector is one aligned LDS vector (a lane's outputs past len are MAX and
+    // land past the chunk)
+    const int64_t out0 = dc->out0;
     const int sh = (int)(out0 & 3);
+    if (pos < len) {
+        uint32_t* q = s + sh + pos;
 #pragma unroll
-    for (int j = 0; j < IT; ++j) s[pos + j < len ? sh + pos + j : DUMP] = r[j];
+        for (int j = 0; j < IT; ++j) q[j] = r[j];
+    }
     __syncthreads();
     const int nv = (sh + len + 3) >> 2;
     uint32_t* __restrict__ o = dst + (out0 - sh);
@@ -433,13 +445,13 @@ template <bool FENCES, int MODE = 0>
 __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_merge4(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                Geo4 geo, const Desc* __restrict__ desc,
                                                uint64_t* __restrict__ fout, int64_t nchunks) {
-    __shared__ __attribute__((aligned(16))) uint32_t s[LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_tile[LDS_WORDS];
+    uint32_t* s = s_tile + PAD;
     const int tid = threadIdx.x;
     int64_t c = blockIdx.x;
     if (c >= nchunks) return;
-    Chunk k = chunk_of(src, geo, desc, c);
     uint32_t x[IT];
-    chunk_loads(k, tid, x);
+    chunk_loads(src, desc + c, tid, x);
     for (;;) {
         // lane id through an opaque copy: lane-derived addresses are recomputed
         // every chunk instead of being hoisted into loop-invariant VGPRs, which
@@ -447,19 +459,14 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_merge4(const uint3
         // prefetch issued before it
         int t = threadIdx.x;
         asm volatile("" : "+v"(t));
-        chunk_to_lds(s, k, t, x);
+        chunk_to_lds(s, desc + c, t, x);
         __syncthreads();
         const int64_t cn = c + gridDim.x;
-        Chunk kn = k;
-        if (cn < nchunks) {
-            kn = chunk_of(src, geo, desc, cn);
-            chunk_loads(kn, t, x);
-        }
-        chunk_merge<FENCES, MODE>(s, k, t, dst, fout, geo.lw + 2);
+        if (cn < nchunks) chunk_loads(src, desc + cn, t, x);
+        chunk_merge<FENCES, MODE>(s, desc + c, t, dst, fout, geo.lw + 2);
         if (cn >= nchunks) break;
         __syncthreads();  // the next chunk overwrites the tile
         c = cn;
-        k = kn;
     }
 }
 
@@ -502,8 +509,8 @@ int64_t merge4_chunks(int64_t n, int lw) {
 hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, hipStream_t s, int phase,
                         bool gather, bool write_next) {
     if (n <= 0) return hipSuccess;
-    // chunks index a group with 32-bit offsets (4W <= 2^32); runs at least CAP long
-    if (lw < 15 || lw > 30 || src == dst) return hipErrorInvalidValue;
+    // load rows address a group with 32-bit byte offsets (4W*4 <= 2^32); runs at least CAP long
+    if (lw < 15 || lw > 28 || src == dst) return hipErrorInvalidValue;
     Geo4 geo{n, lw, 0, 0};
     geo.nfull = n >> (lw + 2);
     geo.kf = ((((int64_t)4 << lw) >> FG_LOG2) + FM - 1) / FM;  // chunks of a full group
@@ -534,7 +541,7 @@ hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, h
         if (e != hipSuccess) return e;
     }
     k_bounds4<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(src, F, M, geo, nslots, bounds);
-    k_chunk_desc<<<(unsigned)((nchunks + 255) / 256), 256, 0, s>>>(bounds, geo, nchunks, desc);
+    k_chunk_desc<<<(unsigned)((nchunks * (NROWS + 1) + 255) / 256), 256, 0, s>>>(bounds, geo, nchunks, desc);
     static int64_t cap = 0;  // resident workgroups (the persistent grid)
     if (cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;

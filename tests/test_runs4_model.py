@@ -11,7 +11,8 @@ FM)) matches the bounds layout."""
 import numpy as np
 import pytest
 
-FG_LOG2, FM = 8, 31
+FG_LOG2, FM = 8, 28
+NT, IT = 256, 36  # k_merge4 lanes and load rows
 FG = 1 << FG_LOG2
 CAP = (FM + 4) * FG
 
@@ -98,6 +99,8 @@ def test_chunks_tile_and_bound(lw, n_groups, tail, kind):
             seg = [x[base + r * W + a[r]: base + r * W + b[r]] for r in range(4)]
             size = sum(s.size for s in seg)
             assert all(b[r] >= a[r] for r in range(4)) and size <= CAP
+            # load rows: each row of NT keys inside one segment, IT rows per chunk
+            assert sum(-(-s.size // NT) for s in seg) <= IT
             chunk = np.sort(np.concatenate(seg))
             if chunk.size and prev_max is not None:
                 assert chunk[0] >= prev_max
