@@ -78,9 +78,9 @@ struct PlanKnobs {
     // 64 MiB) stay on the network, whose passes are shorter there (2^24:
     // 0.60 vs 0.63 ms, 2^20: 0.18 vs 0.21 ms; 2^28: 10.3 vs 6.8 ms).
     int merge_min_log2_u32 = 24;
-    // u32 merge levels in pairs, one 4-way pass per two levels (runs4.hip);
-    // 0: one 2-way pass per level (MISORT_RUNS4)
-    int runs4 = 1;
+    // u32 merge levels: up to this many levels per multi-way pass (runsk.hip,
+    // 2^lk-way); 0 or 1: one 2-way pass per level (MISORT_MULTIWAY)
+    int multiway = 3;
     PlanKnobs();
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
@@ -1372,11 +1372,23 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
     if (runs && m0 > 0 && k > m0 && !(sizeof(K) == 4 && k <= kn.merge_min_log2_u32)) {
         std::vector<Pass> ps = plan_uncached<K, LT, LTR>(m0 < LT ? LT : m0, false);
         int lw = m0 < LT ? LT : m0;
-        // two levels per pass where the 4-way merge applies (u32); an odd
-        // level left over runs last as a 2-way pass (which keeps host
-        // staging's chunked final pass)
-        if (sizeof(K) == 4 && kn.runs4)
-            for (; lw + 2 <= k && lw >= 15 && lw <= 28; lw += 2) ps.push_back(Pass{KIND_RUNS4, lw, 0, false});
+        // u32: the levels in as few multi-way passes as the cap allows (a
+        // pass of lk levels is one HBM sweep; runsk.hip needs lw >= 15 and
+        // lw + lk <= 30), the larger ones first; a single level left over
+        // runs as a 2-way pass (which keeps host staging's chunked final pass)
+        if (sizeof(K) == 4 && kn.multiway >= 2 && lw >= 15) {
+            const int cap = kn.multiway < 3 ? kn.multiway : 3;
+            const int L = (k < 30 ? k : 30) - lw;  // levels the multi-way passes can take
+            if (L >= 2) {
+                const int np = (L + cap - 1) / cap;  // fewest passes
+                for (int i = 0; i < np; ++i) {
+                    // spread the levels: the first L % np passes take one more
+                    const int lk = L / np + (i < L % np ? 1 : 0);
+                    ps.push_back(Pass{KIND_RUNSK, lw, lk, false});
+                    lw += lk;
+                }
+            }
+        }
         for (; lw < k; ++lw) ps.push_back(Pass{KIND_RUNS, lw, 0, false});
         return ps;
     }
@@ -1424,17 +1436,17 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
     const int np = (int)ps.size();
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
-    int fence_phase = 0;  // 4-way passes: fence buffer holding the next pass's fences
+    int fence_phase = 0;  // multi-way passes: fence buffer holding the next pass's fences
     for (int i = 0; i < np; ++i) {
         // ping-pong: pass i writes `out` iff an even number of passes follow it
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
-        if (p.kind == KIND_RUNS4) {
+        if (p.kind == KIND_RUNSK) {
             if constexpr (sizeof(K) == 4) {
-                const bool prev4 = i > 0 && ps[i - 1].kind == KIND_RUNS4;
-                const bool next4 = i + 1 < np && ps[i + 1].kind == KIND_RUNS4;
-                const hipError_t e = merge_level4(src, dst, n, p.hi, s, fence_phase, !prev4, next4);
+                const bool prevk = i > 0 && ps[i - 1].kind == KIND_RUNSK;
+                const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
+                const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next);
                 if (e != hipSuccess) return e;
                 fence_phase ^= 1;
                 src = dst;
@@ -1501,8 +1513,8 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);  // runs of 2^hi -> 2^(hi+1)
-    if (kind == KIND_RUNS4) {  // runs of 2^hi -> 2^(hi+2)
-        if constexpr (sizeof(K) == 4) return merge_level4(in, out, n, hi, s, 0, true, false);
+    if (kind == KIND_RUNSK) {  // runs of 2^hi -> 2^(hi+R), R = 1..3 (0: 2)
+        if constexpr (sizeof(K) == 4) return merge_levelk(in, out, n, hi, R > 0 ? R : 2, s, 0, true, 0);
         return hipErrorInvalidValue;
     }
     if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER ||

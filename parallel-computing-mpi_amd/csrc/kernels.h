@@ -19,7 +19,7 @@ enum Kind : int {
     KIND_WIDE = 6,        // ROWS strides in a 2^16-key register tile (u32)
     KIND_RUNS = 7,        // one merge level: runs of 2^hi keys -> runs of 2^(hi+1)
     KIND_EXCHANGE = 8,    // compare-split exchange leg (samples, RCCL send/recv, codec); not a kernel
-    KIND_RUNS4 = 9,       // two merge levels in one pass: runs of 2^hi -> 2^(hi+2), 4-way (runs4.hip)
+    KIND_RUNSK = 9,       // R merge levels in one pass: runs of 2^hi -> 2^(hi+R), 2^R-way (runsk.hip)
     KIND_COUNT = 10
 };
 
@@ -82,17 +82,18 @@ hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, in
 template <typename K>
 hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0);
 
-// Two merge levels in one HBM pass (runs4.hip, u32): src holds ascending runs of
-// 2^lw keys, dst gets ascending runs of 2^(lw+2) (4-way merge of each group of
-// four runs; the last group may be short).  Chunks are cut at fences (every
-// 512th key of a run): `phase` selects which of two per-stream fence buffers
-// holds this pass's fences; gather = build them from src first (the pass
-// after a non-4-way pass); write_next = write the fences of the next 4-way
-// pass (runs of 2^(lw+2)) into the other buffer.  src != dst; buffers 16-byte
+// lk merge levels in one HBM pass (runsk.hip, u32, lk = 1..3): src holds
+// ascending runs of 2^lw keys, dst gets ascending runs of 2^(lw+lk) (2^lk-way
+// merge of each group of runs; the last group may be short).  Chunks are cut
+// at fences (every 256th key of a run): `phase` selects which of two
+// per-stream fence buffers holds this pass's fences; gather = build them from
+// src first (the pass after a non-multi-way pass); lk_next > 0 = write the
+// fences of the next multi-way pass (runs of 2^(lw+lk), groups of 2^lk_next)
+// into the other buffer.  15 <= lw, lw + lk <= 30; src != dst; buffers 16-byte
 // aligned.
-hipError_t merge_level4(const uint32_t* src, uint32_t* dst, int64_t n, int lw, hipStream_t s, int phase,
-                        bool gather, bool write_next);
-int64_t merge4_chunks(int64_t n, int lw);
+hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                        bool gather, int lk_next);
+int64_t mergek_chunks(int64_t n, int lw, int lk);
 
 // psort.cc:88-101 lower_bound on a sorted device run: *d_out = first i with
 // x <= a[i], or n.

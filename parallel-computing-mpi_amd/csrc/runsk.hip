@@ -1,0 +1,711 @@
+// runsk.hip -- K-way merge passes of the local sort (gfx950, u32 keys):
+// ascending runs of W = 2^lw keys, in groups of K = 2^lk (lk = 1, 2, 3), ->
+// ascending runs of K*W.  One HBM read + one HBM write per key for lk merge
+// levels (runs.hip does one level per pass): 2^30 keys past the 2^15-key SORT
+// tile take five 8-way passes instead of fifteen 2-way ones.
+//
+// The reference's local sort is std::sort (psort.cc:175); any correct sort of
+// payload-free keys writes the same bytes, so the levels past the bitonic SORT
+// tile are merges.  A K-way merge needs, for each output chunk, its start in
+// all K runs.  Exact fixed-size tiles would need a K-way merge-path co-rank
+// per tile (nested searches); instead the chunks are cut at FENCES:
+//
+//   fence   = the key at every FG-th position of a run, packed with its place
+//             as (key << 32 | run-in-group << (32 - lk) | position / FG), so
+//             that u64 order is the total order (key, run, position) -- ties
+//             between equal keys go to the lower run, then the lower position;
+//   chunks  = the fences of a group merged into that total order (k_fence_lds
+//             or lk u64 merge levels), every FM-th one starting a chunk;
+//   bounds  = for a chunk-start fence f of run r0 at position j0*FG, run r0
+//             starts at j0*FG and every other run r at its count of keys
+//             before f, found by a binary search confined to the FG positions
+//             between two of run r's own fences (k_bounds, one thread per
+//             chunk start and run);
+//   rows    = each chunk's loads as rows of RW keys inside one segment: a
+//             byte offset and an LDS word per row (k_chunk_desc), so a load is
+//             a scalar base plus the lane;
+//   merge   = one workgroup per chunk (k_mergek): the K segments are streamed
+//             into LDS, merged pairwise in lk levels in LDS, and stored through
+//             LDS as 16-byte non-temporal stores; the keys at every FG-th
+//             output position are written as the next pass's fences.
+//
+// Between two consecutive chunk starts lie FM fences; run r contributes at
+// most (its fences there + 1) * FG keys, so a chunk holds at most
+// (FM + K) * FG = CAP keys and FM * FG on average.  The first multi-way pass
+// after the SORT tile gathers its fences from the runs (k_fence_gather);
+// later passes read the fences the previous pass wrote.
+#include "kernels.h"
+
+#include <map>
+#include <mutex>
+
+namespace misort {
+namespace {
+
+constexpr int FG_LOG2 = 8;
+constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
+constexpr int CAP = 8192;                       // most keys of a chunk
+#ifndef MISORT_MK_NT
+#define MISORT_MK_NT 512
+#endif
+constexpr int NT = MISORT_MK_NT;         // lanes per chunk workgroup
+constexpr int IT = NT == 256 ? 36 : 18;  // keys per lane
+static_assert(NT == 256 || NT == 512, "chunk workgroup");
+// Every sequence an in-LDS merge reads is followed by G words of MAX
+// (sentinels), so a merge chain needs no end checks: it reads at most IT words
+// past an exhausted sequence.  Each level places its pairs' outputs at lane
+// boundaries past the previous pair's sentinels (no lane straddles two pairs).
+constexpr int G = IT + 1;
+constexpr int PAD = 4;  // words below the tile: a co-rank probe may read index -1
+// 4 tiles of ~34 KiB per CU (LDS); 8 waves per SIMD (<= 64 VGPRs) at NT = 512
+constexpr int WG_PER_CU = 4;
+
+template <int LK>
+struct Shape {
+    static constexpr int K = 1 << LK;
+    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk: 30 / 28 / 24
+    static constexpr int RW = LK == 3 ? 128 : 256;  // load row: RW keys of one segment
+    static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
+    static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
+    static constexpr int LDS_WORDS = PAD + CAP + K * (G + IT) + 16;
+    static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
+    static_assert(CAP + (K / 2) * (G + IT) <= NT * IT, "level layout: pairs at lane boundaries");
+    static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS word of a row fits 16 bits");
+};
+
+typedef uint32_t vec4 __attribute__((ext_vector_type(4)));
+typedef uint32_t vec2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return (uint32_t)(uintptr_t)(const lds_u32*)p; }
+__device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(const lds_u32*)(uintptr_t)a; }
+
+__device__ __host__ __forceinline__ uint64_t fpack(uint32_t key, int64_t gp, int lw, int lk) {
+    const uint64_t r = (uint64_t)(gp >> lw) & ((1u << lk) - 1);
+    const uint64_t j = (uint64_t)(gp & (((int64_t)1 << lw) - 1)) >> FG_LOG2;
+    return ((uint64_t)key << 32) | (r << (32 - lk)) | j;
+}
+
+// Group geometry of the pass: groups of K runs of W keys; run r of group g
+// starts at g*KW + r*W and holds clamp(n - start, 0, W) keys.
+struct Geo {
+    int64_t n;
+    int lw, lk, fm;
+    int64_t nfull;  // full groups
+    int64_t kf;     // chunks per full group
+    __device__ __host__ int K() const { return 1 << lk; }
+    __device__ __host__ int64_t W() const { return (int64_t)1 << lw; }
+    __device__ __host__ int64_t base(int64_t g) const { return g << (lw + lk); }
+    __device__ __host__ int64_t run_len(int64_t g, int r) const {
+        const int64_t rest = n - (base(g) + r * W());
+        return rest <= 0 ? 0 : (rest < W() ? rest : W());
+    }
+    __device__ __host__ int64_t nfences(int64_t g) const {
+        const int64_t glen = (n - base(g)) < K() * W() ? n - base(g) : K() * W();
+        return (glen + FG - 1) >> FG_LOG2;
+    }
+    __device__ __host__ int64_t nchunks(int64_t g) const { return (nfences(g) + fm - 1) / fm; }
+    // bounds slot of chunk t of group g (each group has nchunks + 1 slots)
+    __device__ __host__ int64_t slot(int64_t g, int64_t t) const {
+        return g < nfull ? g * (kf + 1) + t : nfull * (kf + 1) + t;
+    }
+};
+
+Geo make_geo(int64_t n, int lw, int lk) {
+    Geo geo{n, lw, lk, CAP / (int)FG - (1 << lk), 0, 0};
+    geo.nfull = n >> (lw + lk);
+    geo.kf = ((((int64_t)1 << (lw + lk)) >> FG_LOG2) + geo.fm - 1) / geo.fm;
+    return geo;
+}
+
+// F[i] = fence of position i*FG (the first multi-way pass after the SORT tile).
+__global__ void k_fence_gather(const uint32_t* __restrict__ src, int64_t n, int lw, int lk, uint64_t* __restrict__ F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nf = (n + FG - 1) >> FG_LOG2;
+    if (i >= nf) return;
+    const int64_t gp = i << FG_LOG2;
+    F[i] = fpack(src[gp], gp, lw, lk);
+}
+
+// The fences of one group (<= 8192) merged into total order in LDS: each
+// fence's rank = its index in its run's list + its lower bound in the others.
+__global__ __launch_bounds__(1024) void k_fence_lds(const uint64_t* __restrict__ F, uint64_t* __restrict__ M,
+                                                    Geo geo) {
+    extern __shared__ uint64_t sf[];
+    const int64_t g = blockIdx.x;
+    const int64_t f0 = geo.base(g) >> FG_LOG2;
+    const int nfg = (int)geo.nfences(g);
+    const int wf = (int)(geo.W() >> FG_LOG2);  // fences per full run
+    const int K = geo.K();
+    for (int e = threadIdx.x; e < nfg; e += blockDim.x) sf[e] = F[f0 + e];
+    __syncthreads();
+    for (int e = threadIdx.x; e < nfg; e += blockDim.x) {
+        const uint64_t v = sf[e];
+        const int r = e / wf;
+        int rank = e - r * wf;
+        for (int q = 0; q < K; ++q) {
+            if (q == r) continue;
+            int lo = q * wf, hi = (q + 1) * wf < nfg ? (q + 1) * wf : nfg;
+            if (lo >= hi) continue;
+            const int l0 = lo;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (sf[mid] < v) lo = mid + 1;
+                else hi = mid;
+            }
+            rank += lo - l0;
+        }
+        if (rank < nfg) M[f0 + rank] = v;  // always true for well-formed fences
+    }
+}
+
+// Chunk index -> (group, chunk within the group), and the group's first chunk.
+__device__ __forceinline__ void chunk_place(const Geo& geo, int64_t c, int64_t& g, int64_t& t) {
+    if (c < geo.nfull * geo.kf) {
+        g = c / geo.kf;
+        t = c - g * geo.kf;
+    } else {
+        g = geo.nfull;
+        t = c - geo.nfull * geo.kf;
+    }
+}
+
+constexpr int SCAN_NT = 256;  // chunks per block of the fence-count scan
+
+// Inclusive scan of v over the block (SCAN_NT lanes, 4 waves of 64).
+__device__ __forceinline__ int block_scan(int v, int* sw) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        v += lane >= o ? u : 0;
+    }
+    if (lane == 63) sw[w] = v;
+    __syncthreads();
+    for (int q = 0; q < w; ++q) v += sw[q];
+    __syncthreads();
+    return v;
+}
+
+// Fence counts per chunk and run (the chunk's FM fences of the merged order,
+// by their run bits), exclusive-scanned over chunks: blocks of SCAN_NT
+// chunks, P = the scan within the block, bsum = the block totals.  A run's
+// fences before a chunk-start fence = P(c) - P(group's first chunk), with the
+// block totals scanned in (k_scan_totals) -- this replaces a binary search of
+// each run's fence list.
+__global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const uint64_t* __restrict__ M, Geo geo, int64_t nchunks,
+                                                          int* __restrict__ P, int* __restrict__ bsum) {
+    __shared__ int sw[SCAN_NT / 64];
+    const int64_t c = (int64_t)blockIdx.x * SCAN_NT + threadIdx.x;
+    const int K = geo.K();
+    int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < nchunks) {
+        int64_t g, t;
+        chunk_place(geo, c, g, t);
+        const uint64_t* m = M + (geo.base(g) >> FG_LOG2);
+        const int64_t e0 = t * geo.fm, nf = geo.nfences(g);
+        const int64_t e1 = e0 + geo.fm < nf ? e0 + geo.fm : nf;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int r = (int)((m[e] >> (32 - geo.lk)) & (K - 1));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cnt[q] += q == r;
+        }
+    }
+    for (int q = 0; q < K; ++q) {
+        const int inc = block_scan(cnt[q], sw);
+        if (c < nchunks) P[c * K + q] = inc - cnt[q];
+        if (threadIdx.x == SCAN_NT - 1) bsum[(int64_t)blockIdx.x * K + q] = inc;
+    }
+}
+
+// Exclusive scan of the block totals (one workgroup, carried over rounds).
+__global__ __launch_bounds__(SCAN_NT) void k_scan_totals(int* __restrict__ bsum, int64_t nb, int K) {
+    __shared__ int sw[SCAN_NT / 64];
+    __shared__ int tot;
+    for (int q = 0; q < K; ++q) {
+        int carry = 0;
+        for (int64_t b0 = 0; b0 < nb; b0 += SCAN_NT) {
+            const int64_t b = b0 + threadIdx.x;
+            const int v = b < nb ? bsum[b * K + q] : 0;
+            const int inc = block_scan(v, sw);
+            if (b < nb) bsum[b * K + q] = carry + inc - v;
+            if (threadIdx.x == SCAN_NT - 1) tot = inc;
+            __syncthreads();
+            carry += tot;
+            __syncthreads();
+        }
+    }
+}
+
+// One thread per (bounds slot, run): the start of chunk t of group g in run r
+// (a position within the run), or the run's length for the group's end slot.
+// Run r's fences before the chunk-start fence f come from the scanned counts;
+// the keys before f lie among the FG positions after the last of them.
+__global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __restrict__ M,
+                         const int* __restrict__ P, const int* __restrict__ bsum, Geo geo, int64_t nslots,
+                         int64_t* __restrict__ bounds) {
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (nslots << geo.lk)) return;
+    const int64_t s = id >> geo.lk;
+    const int r = (int)(id & (geo.K() - 1));
+    int64_t g, t;
+    if (s < geo.nfull * (geo.kf + 1)) {
+        g = s / (geo.kf + 1);
+        t = s - g * (geo.kf + 1);
+    } else {
+        g = geo.nfull;
+        t = s - geo.nfull * (geo.kf + 1);
+    }
+    const int64_t base = geo.base(g), W = geo.W(), len = geo.run_len(g, r);
+    if (t == geo.nchunks(g)) {
+        bounds[id] = len;
+        return;
+    }
+    const uint64_t f = M[(base >> FG_LOG2) + t * geo.fm];
+    const uint32_t v = (uint32_t)(f >> 32);
+    const int r0 = (int)((f >> (32 - geo.lk)) & (geo.K() - 1));
+    if (r == r0) {
+        bounds[id] = (int64_t)(f & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
+        return;
+    }
+    if (len == 0) {
+        bounds[id] = 0;
+        return;
+    }
+    // fences of run r before f: counts of the group's chunks before chunk t
+    const int K = geo.K();
+    const int64_t c = g * geo.kf + t, c0 = g * geo.kf;  // the tail group starts at nfull * kf too
+    const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / SCAN_NT) * K + r]) -
+                       (P[c0 * K + r] + bsum[(c0 / SCAN_NT) * K + r]);
+    if (lo <= 0) {  // run r's first key comes after f
+        bounds[id] = 0;
+        return;
+    }
+    // keys before f: all of positions <= (lo-1)*FG, none from lo*FG on (a
+    // binary search: 8 dependent loads within one 1 KiB window measured 4x
+    // faster than two rounds of 16 independent ones -- the pass is bound by
+    // the load count, not by their latency)
+    const uint32_t* kr = src + base + r * W;
+    int64_t a = ((lo - 1) << FG_LOG2) + 1, b = (lo << FG_LOG2) < len ? (lo << FG_LOG2) : len;
+    while (a < b) {  // first position after f: key > v (r < r0) or key >= v (r > r0)
+        const int64_t mid = (a + b) >> 1;
+        const uint32_t k = kr[mid];
+        if (r < r0 ? k <= v : k < v) a = mid + 1;
+        else b = mid;
+    }
+    bounds[id] = a;
+}
+
+// Chunk descriptors: for chunk c, its group's base, its output offset, the
+// chunk positions where its K segments start, and its LOAD ROWS.  A chunk is
+// loaded in NROWS rows of RW consecutive keys, each row inside one segment
+// (segment r takes ceil(l_r / RW) rows; the K take <= CAP/RW + K = NROWS):
+// row j = byte offset of its first key from the group base, and how many of
+// its RW keys are real plus the LDS word the first goes to (segment r's keys
+// start at LDS word o_r + r*G, leaving G words for sentinels after each).
+// The tables are stored by part: entry p*IT + j is row j*NR + p, so a wave
+// reads its IT entries as a few wide scalar loads.
+// Validated so that no chunk can address memory outside its group's runs:
+// a bad chunk gets no rows and is left unwritten (the sort then fails its
+// checks).
+template <int LK>
+struct Desc {
+    int64_t gbase, out0;
+    int o[Shape<LK>::K + 1];           // chunk position of segment r; o[K] = chunk length
+    uint32_t off[Shape<LK>::NROWS];  // byte offset of the row's first key from the group base
+    uint32_t la[Shape<LK>::NROWS];   // real keys of the row (0..RW) | LDS word of its first key << 16
+};
+
+// One wave per chunk (DESC_CPB chunks per workgroup): K lanes read and check
+// the chunk's bounds, every lane gets them by shuffles, then the lanes write
+// the table entries.
+constexpr int DESC_CPB = 4;
+template <int LK>
+__global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo,
+                                                             int64_t nchunks, Desc<LK>* __restrict__ desc) {
+    typedef Shape<LK> S;
+    constexpr int K = S::K;
+    const int64_t c = (int64_t)blockIdx.x * DESC_CPB + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunks) return;  // whole waves
+    int64_t g, t;
+    chunk_place(geo, c, g, t);
+    const int64_t* b0 = bounds + K * geo.slot(g, t);
+    int64_t st = 0, ln = 0;
+    bool ok = true;
+    if (lane < K) {
+        st = b0[lane];
+        ln = b0[K + lane] - st;
+        ok = st >= 0 && ln >= 0 && st + ln <= geo.run_len(g, lane) && ln <= CAP;
+    }
+    // bounds outside the runs would be a logic error: never let them address memory
+    ok = __all(ok);
+    int sln[K], srow[K + 1], so[K + 1];
+    int64_t out = geo.base(g);
+    int tot = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        sln[r] = __shfl((int)ln, r, 64);
+        tot += sln[r];
+    }
+    ok = ok && tot <= CAP;
+    int R = 0, o = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        if (!ok) sln[r] = 0;
+        srow[r] = R;
+        so[r] = o;
+        R += (sln[r] + S::RW - 1) / S::RW;
+        o += sln[r];
+    }
+    srow[K] = R;
+    so[K] = o;
+    const int64_t stl = ok ? st : 0;
+    Desc<LK>& d = desc[c];
+    int64_t sum = stl;  // out0 = group base + sum of the segment starts
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    if (lane == 0) {
+        d.gbase = geo.base(g);
+        d.out0 = out + sum;
+    }
+#pragma unroll
+    for (int r = 0; r <= K; ++r)
+        if (lane == r) d.o[r] = so[r];
+    int64_t sst[K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) sst[r] = __shfl(stl, r, 64);  // all lanes active
+    for (int j = lane; j < S::NROWS; j += 64) {
+        const int row = (j % IT) * S::NR + j / IT;  // table entry j (stored by part)
+        uint32_t off = 0, la = 0;                   // rows past the chunk: no keys
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            if (row >= srow[r] && row < srow[r + 1]) {
+                const int k = row - srow[r];
+                const int rem = sln[r] - k * S::RW;
+                off = (uint32_t)((((int64_t)r << geo.lw) + sst[r] + (int64_t)k * S::RW) * 4);  // < KW*4 <= 2^32
+                la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(so[r] + r * G + k * S::RW) << 16);
+            }
+        }
+        d.off[j] = off;
+        d.la[j] = la;
+    }
+}
+
+// Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
+// (every A key before it <= every B key after it and vice versa; any such
+// split gives the same output values -- the keys carry no payload).  The
+// largest base in [lo, hi] with A[i - 1] <= B[d - i] for every i <= base, by
+// 13 power-of-two steps (hi - lo <= min(LA, LB) <= CAP/2 = 2^12) with clamped
+// probes: no loop control, no branches.  Probe addresses stay inside
+// [A0 - 1, A0 + LA) and [B0, B0 + LB].
+__device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d) {
+    static_assert(CAP / 2 <= 8191, "co-rank steps");
+    const int lo = d - LB > 0 ? d - LB : 0;
+    const int hi = d < LA ? d : LA;
+    const uint32_t* a = s + A0 - 1;
+    const uint32_t* b = s + B0 + d;
+    int base = lo;
+#pragma unroll
+    for (int step = 4096; step >= 1; step >>= 1) {
+        const int i = base + step;
+        const int ic = i < hi ? i : hi;
+        const bool ok = i <= hi && a[ic] <= b[-ic];
+        base = ok ? i : base;
+    }
+    return base;
+}
+
+// IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
+// both followed by sentinels.  A chain holds h, the head of the side it took
+// last, and g, the other side's head: each step outputs min(h, g), keeps
+// max(h, g) as the other head and reads the next key of the side it took
+// (swapping the two read pointers when that side changes) -- six VALU ops and
+// one LDS read per output.  Ties may go either way: equal keys are identical.
+// Past the end of both sequences a chain outputs MAX (their sentinels).
+__device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d,
+                                            uint32_t (&r)[IT]) {
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
+    const int ia = co_rank(s, A0, LA, B0, LB, dc);
+    // byte addresses of the two heads (LDS pointers are 32-bit)
+    uint32_t px = lds_addr(s + A0 + ia), py = lds_addr(s + B0 + dc - ia);
+    uint32_t h = lds_ld(px), g = lds_ld(py);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const bool keep = h <= g;
+        r[k] = min(h, g);
+        const uint32_t o = max(h, g);
+        const uint32_t nx = keep ? px : py;
+        py = keep ? py : px;
+        px = nx + 4;
+        h = lds_ld(px);
+        g = o;
+    }
+}
+
+// The wave's row part (uniform) and the lane's place in its row.
+template <int LK>
+__device__ __forceinline__ int row_part(int tid) { return __builtin_amdgcn_readfirstlane(tid) / Shape<LK>::RW; }
+
+// k_mergek: one workgroup per chunk.  MODE (probes only, MISORT_MK_PROBE):
+// 0 = the pass; 1 = no merge (the access pattern's floor); 2 = level 1 only.
+// Waves whose lanes all lie past a level's outputs skip its merge (a chunk
+// averages FM*FG of CAP keys).
+template <int LK, bool FENCES, int MODE = 0>
+__global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint32_t* __restrict__ src,
+                                                                      uint32_t* __restrict__ dst,
+                                                                      const Desc<LK>* __restrict__ desc,
+                                                                      uint64_t* __restrict__ fout, int lwn, int lkn) {
+    typedef Shape<LK> S;
+    constexpr int K = S::K;
+    constexpr int LAST = S::LDS_WORDS - PAD - 1;
+    __shared__ __attribute__((aligned(16))) uint32_t tile[S::LDS_WORDS];
+    uint32_t* s = tile + PAD;
+    const int tid = threadIdx.x;
+    const Desc<LK>* d = desc + blockIdx.x;
+    {
+        // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
+        // table entries first (scalar registers), then all its loads
+        const char* gsrc = (const char*)(src + d->gbase);
+        const int part = row_part<LK>(tid), lt = tid & (S::RW - 1);
+        const uint32_t* offp = d->off + part * IT;
+        const uint32_t* lap = d->la + part * IT;
+        uint32_t off[IT], la[IT], x[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            off[j] = offp[j];
+            la[j] = lap[j];
+        }
+#pragma unroll
+        for (int j = 0; j < IT; ++j)
+            if (lt < (int)(la[j] & 0xFFFF))
+                x[j] = __builtin_nontemporal_load((const uint32_t*)(gsrc + off[j]) + (uint32_t)lt);
+#pragma unroll
+        for (int j = 0; j < IT; ++j)
+            if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
+        if (tid < K * G) {  // the sentinels after every segment
+            const int r = tid / G;
+            s[d->o[r + 1] + r * G + (tid - r * G)] = 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    const int len = d->o[K];
+    uint32_t r[IT];
+    const int pos = tid * IT;
+    const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
+    // the current level's input sequences (uniform): start and length
+    int st[K], ln[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        st[q] = d->o[q] + q * G;
+        ln[q] = d->o[q + 1] - d->o[q];
+    }
+#pragma unroll
+    for (int lv = 1; lv <= LK; ++lv) {
+        const int P = K >> lv;  // pairs merged at this level
+        // pair p's output: [qp[p], qp[p] + lp[p]), then G sentinels; the next
+        // pair starts at the first lane boundary past them
+        int qp[K / 2], lp[K / 2];
+        int qa = 0;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            lp[p] = ln[2 * p] + ln[2 * p + 1];
+            qp[p] = qa;
+            qa = (qa + lp[p] + G + IT - 1) / IT * IT;
+        }
+        // the lane's pair: the last one starting at or before pos
+        int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
+#pragma unroll
+        for (int p = 1; p < P; ++p) {
+            const bool in = pos >= qp[p];
+            A0 = in ? st[2 * p] : A0;
+            LA = in ? ln[2 * p] : LA;
+            B0 = in ? st[2 * p + 1] : B0;
+            LB = in ? ln[2 * p + 1] : LB;
+            Q = in ? qp[p] : Q;
+            LP = in ? lp[p] : LP;
+        }
+        const int end = qp[P - 1] + lp[P - 1];
+        if (MODE == 1 || (MODE == 2 && lv > 1)) {
+#pragma unroll
+            for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
+        } else if (wpos < end) {
+            merge_chain(s, A0, LA, B0, LB, pos - Q, r);
+        }
+        __syncthreads();
+        if (lv < LK) {
+            // a lane's outputs past its pair's end are MAX (the chain ran into
+            // the sentinels), the value the sentinel stores write there too
+            if (pos < Q + LP) {
+#pragma unroll
+                for (int j = 0; j < IT; j += 2) *reinterpret_cast<vec2*>(s + pos + j) = vec2{r[j], r[j + 1]};
+            }
+            if (tid < P * G) {
+                const int p = tid / G;
+                int e = 0;
+#pragma unroll
+                for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
+                s[e + (tid - p * G)] = 0xFFFFFFFFu;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                st[p] = qp[p];
+                ln[p] = lp[p];
+            }
+        }
+    }
+    // the chunk goes to LDS shifted by out0 mod 4, so every global 16-byte
+    // vector is one aligned LDS vector (a lane's outputs past len are MAX and
+    // land past the chunk)
+    const int64_t out0 = d->out0;
+    const int sh = (int)(out0 & 3);
+    if (pos < len) {
+        uint32_t* q = s + sh + pos;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) q[j] = r[j];
+    }
+    __syncthreads();
+    const int nv = (sh + len + 3) >> 2;
+    uint32_t* __restrict__ o = dst + (out0 - sh);
+    for (int v = tid; v < nv; v += NT) {
+        const int e = 4 * v;
+        if (e >= sh && e + 4 <= sh + len) {
+            __builtin_nontemporal_store(*reinterpret_cast<const vec4*>(s + e), reinterpret_cast<vec4*>(o + e));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (e + j >= sh && e + j < sh + len) o[e + j] = s[e + j];
+        }
+    }
+    if constexpr (FENCES) {
+        // the chunk's fences are consecutive entries of fout: one coalesced
+        // 8-byte store per fence from consecutive lanes
+        const int64_t first = (out0 + FG - 1) & ~(FG - 1);
+        const int nf = first < out0 + len ? (int)((out0 + len - first + FG - 1) >> FG_LOG2) : 0;
+        if (tid < nf) {
+            const int64_t gp = first + ((int64_t)tid << FG_LOG2);
+            fout[gp >> FG_LOG2] = fpack(s[(int)(gp - (out0 - sh))], gp, lwn, lkn);
+        }
+    }
+}
+
+// Fence buffers, bounds and descriptors: one grow-only set per (device, stream).
+struct Scratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_mu;
+std::map<std::pair<int, hipStream_t>, Scratch> g_scr;
+
+void* scratch(size_t bytes, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto& e = g_scr[{dev, s}];
+    if (e.bytes < bytes) {
+        if (e.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(e.p) != hipSuccess)) return nullptr;
+        e = Scratch{};
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        e = Scratch{p, bytes};
+    }
+    return e.p;
+}
+
+int64_t chunks_of(const Geo& geo) {
+    const bool tail = (geo.nfull << (geo.lw + geo.lk)) < geo.n;
+    return geo.nfull * geo.kf + (tail ? geo.nchunks(geo.nfull) : 0);
+}
+
+template <int LK>
+hipError_t merge_pass(const uint32_t* src, uint32_t* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
+                      int lk_next) {
+    typedef Shape<LK> S;
+    const Geo geo = make_geo(n, lw, LK);
+    const bool tail = (geo.nfull << (lw + LK)) < n;
+    const int64_t nchunks = chunks_of(geo);
+    const int64_t nslots = geo.nfull * (geo.kf + 1) + (tail ? geo.nchunks(geo.nfull) + 1 : 0);
+    const int64_t nf = (n + FG - 1) >> FG_LOG2;
+    if (nchunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    // layout: fence buffers 0 and 1, merged fences, u64 merge temp, bounds,
+    // fence counts and their block totals, descriptors
+    const int64_t nbk = (nchunks + SCAN_NT - 1) / SCAN_NT;
+    const size_t fb = ((size_t)nf * 8 + 255) & ~(size_t)255;
+    const size_t bb = ((size_t)nslots * S::K * 8 + 255) & ~(size_t)255;
+    const size_t cb = ((size_t)nbk * SCAN_NT * S::K * 4 + 255) & ~(size_t)255;
+    const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
+    char* base = (char*)scratch(4 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<LK>) + 256, s);
+    if (!base) return hipErrorOutOfMemory;
+    int* cnt = (int*)(base + 4 * fb + bb);
+    int* bsum = (int*)(base + 4 * fb + bb + cb);
+    uint64_t* F = (uint64_t*)(base + (phase & 1) * fb);
+    uint64_t* Fn = (uint64_t*)(base + ((phase & 1) ^ 1) * fb);
+    uint64_t* M = (uint64_t*)(base + 2 * fb);
+    uint64_t* T = (uint64_t*)(base + 3 * fb);
+    int64_t* bounds = (int64_t*)(base + 4 * fb);
+    Desc<LK>* desc = (Desc<LK>*)(base + 4 * fb + bb + cb + sb);
+    if (gather) k_fence_gather<<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
+    const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
+    if (wf_log2 + LK <= 13) {          // group fences <= 8192: 64 KiB of LDS
+        const int ngroups = (int)(geo.nfull + (tail ? 1 : 0));
+        const size_t lds = ((size_t)1 << (wf_log2 + LK)) * 8;
+        k_fence_lds<<<ngroups, 1024, lds, s>>>(F, M, geo);
+    } else {
+        // LK u64 merge levels landing in M: F -> M; F -> T -> M; F -> M -> T -> M
+        const uint64_t* a = F;
+        for (int l = 0; l < LK; ++l) {
+            uint64_t* b = ((LK - 1 - l) & 1) ? T : M;
+            const hipError_t e = merge_level<uint64_t>(a, b, nf, wf_log2 + l, s);
+            if (e != hipSuccess) return e;
+            a = b;
+        }
+    }
+    const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
+    k_fence_counts<<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
+    k_bounds<<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, M, cnt, bsum, geo, nslots, bounds);
+    k_chunk_desc<LK><<<(unsigned)((nchunks + DESC_CPB - 1) / DESC_CPB), 64 * DESC_CPB, 0, s>>>(bounds, geo, nchunks,
+                                                                                             desc);
+    const unsigned grid = (unsigned)nchunks;
+    if (lk_next > 0) k_mergek<LK, true><<<grid, NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
+    else k_mergek<LK, false><<<grid, NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
+    static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
+    if (probe) {
+        // same chunks, outputs to a scratch buffer (the sort is untouched)
+        static uint32_t* junk = nullptr;
+        static size_t junk_n = 0;
+        if (junk_n < (size_t)n) {
+            if (junk) (void)hipFree(junk);
+            junk = nullptr;
+            if (hipMalloc(&junk, (size_t)n * 4) != hipSuccess) return hipErrorOutOfMemory;
+            junk_n = (size_t)n;
+        }
+        k_mergek<LK, false, 1><<<grid, NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+        k_mergek<LK, false, 2><<<grid, NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+int64_t mergek_chunks(int64_t n, int lw, int lk) { return chunks_of(make_geo(n, lw, lk)); }
+
+// phase: which of the two fence buffers holds this pass's input fences
+// (gather: build them from src first); lk_next > 0: write the next multi-way
+// pass's fences (runs of 2^(lw+lk) in groups of 2^lk_next) into the other
+// buffer.
+hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                        bool gather, int lk_next) {
+    if (n <= 0) return hipSuccess;
+    // load rows address a group with 32-bit byte offsets (KW*4 <= 2^32); runs
+    // at least a 2^15 SORT tile long
+    if (lk < 1 || lk > 3 || lw < 15 || lw + lk > 30 || src == dst || lk_next < 0 || lk_next > 3)
+        return hipErrorInvalidValue;
+    if (lk == 1) return merge_pass<1>(src, dst, n, lw, s, phase, gather, lk_next);
+    if (lk == 2) return merge_pass<2>(src, dst, n, lw, s, phase, gather, lk_next);
+    return merge_pass<3>(src, dst, n, lw, s, phase, gather, lk_next);
+}
+
+}  // namespace misort

@@ -1309,7 +1309,7 @@ int misort_pass_probe(misort_ctx* c, int dtype, const void* in, void* out, int64
         return fail(MISORT_E_INVALID, "bad pass_probe arguments");
     if (kind != misort::KIND_TILE_SORT && kind != misort::KIND_GLOBAL && kind != misort::KIND_SPAN &&
         kind != misort::KIND_TILE_MERGE && kind != misort::KIND_WIDE && kind != misort::KIND_RUNS &&
-        kind != misort::KIND_RUNS4)
+        kind != misort::KIND_RUNSK)
         return fail(MISORT_E_INVALID, "bad pass kind");
     hipStream_t s = c->stream;
     hipEvent_t e0, e1;

@@ -1,7 +1,7 @@
 """GPU parity of the merge levels (runs.hip) -- the passes that finish the
 local sort replacing the reference's std::sort (psort.cc:175) once runs leave
-the SORT tile: 2-way levels (runs.hip) and 4-way passes of two levels each
-(runs4.hip).
+the SORT tile: 2-way levels (runs.hip) and 2^lk-way passes of lk levels each
+(runsk.hip, lk = 1..3).
 
 * One merge level (misort_pass_probe, kind run_merge) on inputs made of
   ascending runs of 2^hi keys, ragged tails included, is compared bit for bit
@@ -57,21 +57,21 @@ def expect(x, hi):
     return out
 
 
-def expect4(x, hi):
+def expectk(x, hi, lk):
     out = x.copy()
-    w4 = 4 << hi
-    for s in range(0, x.size, w4):
-        out[s:s + w4].sort()
+    wk = 1 << (hi + lk)
+    for s in range(0, x.size, wk):
+        out[s:s + wk].sort()
     return out
 
 
-def run_level(ctx, x, hi, kind="run_merge"):
+def run_level(ctx, x, hi, kind="run_merge", lk=0):
     if x.dtype == np.uint32:
         d_in = torch.from_numpy(x.view(np.int32)).cuda().view(U32_T)
     else:
         d_in = torch.from_numpy(x.view(np.int64)).cuda().view(U64_T)
     d_out = torch.empty_like(d_in)
-    ctx.pass_probe(d_in, d_out, kind, hi, 0, False, reps=1)
+    ctx.pass_probe(d_in, d_out, kind, hi, lk, False, reps=1)
     torch.cuda.synchronize()
     if x.dtype == np.uint32:
         return d_out.view(torch.int32).cpu().numpy().view(np.uint32)
@@ -96,32 +96,35 @@ def test_merge_level_duplicates_and_single_run(ctx, dt):
         np.testing.assert_array_equal(run_level(ctx, x, hi), expect(x, hi))
 
 
+@pytest.mark.parametrize("lk", [1, 2, 3])
 @pytest.mark.parametrize("hi", [15, 16, 17])
-@pytest.mark.parametrize("n", [(1 << 19), (1 << 19) - 4097, (1 << 18) + 3, 3 * (1 << 17) + 5, 5000, 12345, 2049])
-def test_merge4_level_matches_numpy(ctx, hi, n):
-    """One 4-way pass (runs4.hip): groups of four runs merged, ragged last group
-    (1 to 4 runs, the last one short), fences gathered from the runs."""
-    x = runs_input(n, hi, np.uint32, n + hi)
-    np.testing.assert_array_equal(run_level(ctx, x, hi, "run_merge4"), expect4(x, hi))
+@pytest.mark.parametrize("n", [(1 << 20) + 3, (1 << 19), (1 << 19) - 4097, 3 * (1 << 17) + 5, 5000, 12345, 2049])
+def test_mergek_level_matches_numpy(ctx, lk, hi, n):
+    """One 2^lk-way pass (runsk.hip): groups of 2^lk runs merged, ragged last
+    group (1 to 2^lk runs, the last one short), fences gathered from the runs."""
+    x = runs_input(n, hi, np.uint32, n + hi + lk)
+    np.testing.assert_array_equal(run_level(ctx, x, hi, "run_mergek", lk), expectk(x, hi, lk))
 
 
+@pytest.mark.parametrize("lk", [1, 2, 3])
 @pytest.mark.parametrize("hi", [15, 16, 21])
-def test_merge4_level_ties_and_edges(ctx, hi):
+def test_mergek_level_ties_and_edges(ctx, lk, hi):
     """Duplicate-heavy, all-equal (every fence the same key: chunks cut by
     (run, position)), presorted and interleaved runs; hi = 21 merges the
-    fences with two u64 merge levels instead of in LDS."""
-    n = (4 << hi) + (3 << hi) + 1000  # one full group + a 3-run tail
+    fences with lk u64 merge levels instead of in LDS."""
+    K = 1 << lk
+    n = (K << hi) + ((K - 1) << hi) + 1000  # one full group + a (K-1)-run tail
     cases = [runs_input(n, hi, np.uint32, hi, dup=True), np.full(n, 7, np.uint32),
              np.arange(n, dtype=np.uint32), np.full(n, 0xFFFFFFFF, np.uint32)]
-    inter = np.arange(n, dtype=np.uint32)  # run r holds r, r+4, r+8, ... of its group
+    inter = np.arange(n, dtype=np.uint32)  # run r holds r, r+K, r+2K, ... of its group
     w = 1 << hi
-    for g in range(0, n, 4 * w):
-        for r in range(4):
+    for g in range(0, n, K * w):
+        for r in range(K):
             seg = inter[g + r * w: g + (r + 1) * w]
-            seg[:] = np.arange(seg.size, dtype=np.uint32) * 4 + r
+            seg[:] = np.arange(seg.size, dtype=np.uint32) * K + r
     cases.append(inter)
     for x in cases:
-        np.testing.assert_array_equal(run_level(ctx, x, hi, "run_merge4"), expect4(x, hi))
+        np.testing.assert_array_equal(run_level(ctx, x, hi, "run_mergek", lk), expectk(x, hi, lk))
 
 
 def test_merge_level_rejects_bad_shapes(ctx):
@@ -129,9 +132,9 @@ def test_merge_level_rejects_bad_shapes(ctx):
     for hi in (5, 11):  # runs shorter than the merge tile
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi)
-    for hi in (11, 14):  # 4-way: runs shorter than a chunk
+    for hi, lk in ((11, 2), (14, 2), (15, 4)):  # multi-way: runs shorter than a SORT tile; lk > 3
         with pytest.raises(misort.MisortError):
-            run_level(ctx, x, hi, "run_merge4")
+            run_level(ctx, x, hi, "run_mergek", lk)
 
 
 CHILD = r"""
@@ -161,8 +164,8 @@ a = out.view(iv).cpu().numpy().view(dt)
 b = d.view(iv).cpu().numpy().view(dt)
 ref = np.sort(keys)
 ok = np.array_equal(a, ref) and np.array_equal(b, ref)
-print("RUNS", sum(1 for p in plan if p[0] == "run_merge") + 2 * sum(1 for p in plan if p[0] == "run_merge4"),
-      "RUNS4", sum(1 for p in plan if p[0] == "run_merge4"), "OK" if ok else "MISMATCH")
+print("RUNS", sum(1 for p in plan if p[0] == "run_merge") + sum(p[2] for p in plan if p[0] == "run_mergek"),
+      "RUNSK", sum(1 for p in plan if p[0] == "run_mergek"), "OK" if ok else "MISMATCH")
 ctx.close()
 """
 
@@ -174,8 +177,10 @@ ctx.close()
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_IT": "32"}, (1 << 21) + 77),
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "256"}, (1 << 21) + 77),
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUNS4": "0"}, (1 << 22) + 4099),
-    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 26) + 12345),  # chained 4-way passes, u64 fence merges
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
+    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
+    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
     (4, {"MISORT_MERGE_FROM": "15"}, 3 * (1 << 23) + 5),
     (4, {"MISORT_MERGE_FROM": "15"}, (1 << 17) + 1),
     (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),
@@ -189,12 +194,13 @@ def test_full_sort_merge_from(kb, env, n):
                        text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
-    _, count, _, count4, verdict = line.split()
+    _, count, _, countk, verdict = line.split()
     assert verdict == "OK", line
-    if kb == 4 and env.get("MISORT_RUNS4") != "0" and int(count) >= 2:
-        assert int(count4) == int(count) // 2  # levels in pairs; an odd one left as a 2-way pass
+    cap = int(env.get("MISORT_MULTIWAY", "3"))
+    if kb == 4 and cap >= 2 and int(count) >= 2:
+        assert int(countk) == -(-int(count) // cap)  # the fewest multi-way passes
     else:
-        assert int(count4) == 0
+        assert int(countk) == 0
     m0 = int(next(iter(env.values())))
     if m0 == 0:
         assert int(count) == 0

@@ -15,15 +15,15 @@ import misort
 KIND_SORT, KIND_ROWS, KIND_MERGE, KIND_SPAN = "tile_sort", "global_pass", "tile_merge", "span_pass"
 KIND_WIDE = "wide_pass"  # ROWS stages in the 2^16-key register tile (u32)
 KIND_RUNS = "run_merge"  # one merge level (runs.hip): runs of 2^hi -> 2^(hi+1)
-KIND_RUNS4 = "run_merge4"  # two merge levels in one pass (runs4.hip): runs of 2^hi -> 2^(hi+2)
-MERGES = (KIND_RUNS, KIND_RUNS4)
+KIND_RUNSK = "run_mergek"  # R merge levels in one pass (runsk.hip): runs of 2^hi -> 2^(hi+R)
+MERGES = (KIND_RUNS, KIND_RUNSK)
 
 
 def merge_levels(runs):
     """Levels (input run log2) the merge passes finish, in order."""
     out = []
-    for kind, hi, _, _ in runs:
-        out += [hi, hi + 1] if kind == KIND_RUNS4 else [hi]
+    for kind, hi, r, _ in runs:
+        out += list(range(hi, hi + r)) if kind == KIND_RUNSK else [hi]
     return out
 
 
@@ -92,12 +92,12 @@ def replay(keys, plan, lt):
             stage(x, m, b)
     for m, b in plan_stages(plan, lt):
         stage(x, m, b)
-    for kind, hi, _, _ in split_runs(plan)[1]:
+    for kind, hi, r, _ in split_runs(plan)[1]:
         # merge pass: every run of 2^hi is sorted, each pair (2-way) or group of
-        # four runs (4-way) is merged
+        # 2^r runs (multi-way) is merged
         runs = x.reshape(-1, 1 << hi)
         assert np.all(runs[:, 1:] >= runs[:, :-1])
-        up = 2 if kind == KIND_RUNS4 else 1
+        up = r if kind == KIND_RUNSK else 1
         x = np.sort(x.reshape(-1, 1 << (hi + up)), axis=1).reshape(-1)
     return x[: keys.size]
 
@@ -124,13 +124,17 @@ def test_plan_covers_network(n, key_bytes):
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + seven 4-way passes (levels 16..29 in pairs) + one
-    # 2-way pass for level 30 (one merge pass per level: 1 + 15; the network
-    # alone needs 1 + 28 with wide ROWS passes, 1 + 29 without)
-    assert len(misort.plan(1 << 30, 4)) == 9
-    assert [q[0] for q in misort.plan(1 << 30, 4)] == [KIND_SORT] + [KIND_RUNS4] * 7 + [KIND_RUNS]
-    assert len(misort.plan(1 << 28, 4)) == 8
-    assert [q[0] for q in misort.plan(1 << 29, 4)] == [KIND_SORT] + [KIND_RUNS4] * 7
+    # 2^30 u32: 1 SORT + five 8-way passes (levels 16..30, three per pass; one
+    # 2-way merge pass per level would be 1 + 15; the network alone needs
+    # 1 + 28 with wide ROWS passes, 1 + 29 without)
+    p30 = misort.plan(1 << 30, 4)
+    assert p30[0][0] == KIND_SORT
+    assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 15 + 3 * i, 3) for i in range(5)]
+    # 13 and 14 levels: five passes, the levels spread 3,3,3,2,2 / 3,3,3,3,2
+    assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [3, 3, 3, 2, 2]
+    assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [3, 3, 3, 3, 2]
+    # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
+    assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
     assert len(misort.plan(1 << 24, 4)) == 15  # cache-resident u32 sizes stay on the network
     # u64: 2^13-key SORT tiles, then merge levels
     assert len(misort.plan((1 << 29) - 3, 8)) == 1 + 29 - 13

@@ -5,7 +5,7 @@ i=0
 for set in "SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" \
            "SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAVES"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "${REGEX:-k_merge4}" -d "$OUT/p$i" -o p$i --output-format csv -- \
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "${REGEX:-k_mergek}" -d "$OUT/p$i" -o p$i --output-format csv -- \
     python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-events $BENCH_ARGS > "$OUT/p$i.log" 2>&1 \
     || { echo "pass $i failed"; tail -3 "$OUT/p$i.log"; exit 1; }
 done

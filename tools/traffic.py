@@ -11,10 +11,10 @@ per level.  Their loads are 4 B per lane, not 16 B; FETCH_SIZE still reports hal
 there (k_runs_merge reads every key exactly once: raw 2.197e9 vs 4.295e9 read
 at 2^30, profiles/r01/pmc30_v11/), so the same doubling applies.  The raw value
 is kept as "read_bytes_raw" and the factor as "fetch_scale".
-The 4-way merge pass (runs4.hip) is k_merge4 plus its small planning kernels
-(k_fence_gather on the first 4-way pass, k_fence_lds, k_bounds4, k_chunk_desc);
-"run_merge4" sums them per launch of k_merge4.  k_merge4's loads are 4 B per
-lane too, so the same doubling applies.
+The multi-way merge pass (runsk.hip) is k_mergek plus its small planning
+kernels (k_fence_gather on the first multi-way pass, k_fence_lds or the u64
+fence merge levels, k_bounds, k_chunk_desc); "run_mergek" sums them per launch
+of k_mergek.  k_mergek's loads are 4 B per lane too, so the same doubling applies.
     WORKLOAD=u32_2e30_n1 tools/traffic.py gpurun_out/pmc30 > profiles/traffic.json
 ("workload" must match bench.py's f"{dtype}_2e{logn}_n{ranks}" for bench to use it).
 """
@@ -38,15 +38,15 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
         elif "k_rows_wide" in name:
             fam = "wide_pass"
         elif re.search(r"k_runs_\w+<unsigned long", name):
-            fam = "run4_plan"  # the 64-bit fence merges of a 4-way pass (u32 sorts)
+            fam = "runk_plan"  # the 64-bit fence merges of a multi-way pass (u32 sorts)
         elif "k_runs_merge" in name:
             fam = "run_merge_kernel"
         elif "k_runs_partition" in name:
             fam = "run_partition"
-        elif "k_merge4" in name:
-            fam = "run_merge4_kernel"
-        elif re.search(r"k_fence_gather|k_fence_lds|k_bounds4|k_chunk_desc", name):
-            fam = "run4_plan"
+        elif "k_mergek" in name:
+            fam = "run_mergek_kernel"
+        elif re.search(r"k_fence_gather|k_fence_lds|k_bounds|k_chunk_desc", name):
+            fam = "runk_plan"
         else:
             continue
         acc[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -69,15 +69,15 @@ if "run_merge_kernel" in out and "run_partition" in out:
                                                  "bytes_per_launch", "read_bytes_raw")}
     out["run_merge"].update(launches=a["launches"], fetch_scale=SCALE)
     out["run_merge"]["note"] = "per level: k_runs_merge + k_runs_partition"
-if "run_merge4_kernel" in out:
-    a = out["run_merge4_kernel"]
-    b = out.get("run4_plan")
+if "run_mergek_kernel" in out:
+    a = out["run_mergek_kernel"]
+    b = out.get("runk_plan")
     m = dict(a)
-    if b:  # the planning kernels' bytes, spread over the k_merge4 launches
+    if b:  # the planning kernels' bytes, spread over the k_mergek launches
         for k in ("read_bytes_per_launch", "write_bytes_per_launch", "bytes_per_launch", "read_bytes_raw"):
             if a.get(k) is not None and b.get(k) is not None:
                 m[k] = a[k] + b[k] * b["launches"] / a["launches"]
-    m["note"] = "per 4-way pass: k_merge4 + its planning kernels (fences, bounds, descriptors)"
-    out["run_merge4"] = m
+    m["note"] = "per multi-way pass: k_mergek + its planning kernels (fences, bounds, descriptors)"
+    out["run_mergek"] = m
 json.dump(out, sys.stdout, indent=1)
 print()
