@@ -28,16 +28,21 @@ import sys
 
 FAMILY = {"0": "tile_sort", "1": "tile_merge", "2": "global_pass", "3": "span_pass"}
 root = sys.argv[1]
+# u32 sorts: k_runs_* on unsigned long are the multi-way passes' fence merges;
+# u64 sorts: they are the sort's own merge levels
+U32 = not (os.environ.get("WORKLOAD") or "").startswith("u64")
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
-        m = re.search(r"k_stream<unsigned int, (\d+), (\d)", name)
+        m = re.search(r"k_stream<unsigned (?:int|long), (\d+), (\d)", name)
         if m:
             fam = FAMILY[m.group(2)]
+        elif "k_sort_u32" in name:
+            fam = "tile_sort"
         elif "k_rows_wide" in name:
             fam = "wide_pass"
-        elif re.search(r"k_runs_\w+<unsigned long", name):
+        elif U32 and re.search(r"k_runs_\w+<unsigned long", name):
             fam = "runk_plan"  # the 64-bit fence merges of a multi-way pass (u32 sorts)
         elif "k_runs_merge" in name:
             fam = "run_merge_kernel"
