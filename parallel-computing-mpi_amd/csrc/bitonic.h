@@ -79,7 +79,9 @@ struct PlanKnobs {
     // 0.60 vs 0.63 ms, 2^20: 0.18 vs 0.21 ms; 2^28: 10.3 vs 6.8 ms).
     int merge_min_log2_u32 = 24;
     // u32 merge levels: up to this many levels per multi-way pass (runsk.hip,
-    // 2^lk-way); 0 or 1: one 2-way pass per level (MISORT_MULTIWAY)
+    // 2^lk-way, lk <= 4); 0 or 1: one 2-way pass per level (MISORT_MULTIWAY).
+    // 3 measured best at 2^30: 63.8 Gkeys/s vs 62.6 with 16-way passes (a 4th
+    // in-LDS level and 16-way planning cost more than the pass they save)
     int multiway = 3;
     PlanKnobs();
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
@@ -1377,7 +1379,7 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
         // lw + lk <= 30), the larger ones first; a single level left over
         // runs as a 2-way pass (which keeps host staging's chunked final pass)
         if (sizeof(K) == 4 && kn.multiway >= 2 && lw >= 15) {
-            const int cap = kn.multiway < 3 ? kn.multiway : 3;
+            const int cap = kn.multiway < 4 ? kn.multiway : 4;
             const int L = (k < 30 ? k : 30) - lw;  // levels the multi-way passes can take
             if (L >= 2) {
                 const int np = (L + cap - 1) / cap;  // fewest passes

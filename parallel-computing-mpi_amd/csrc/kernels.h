@@ -82,10 +82,10 @@ hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, in
 template <typename K>
 hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0);
 
-// lk merge levels in one HBM pass (runsk.hip, u32, lk = 1..3): src holds
+// lk merge levels in one HBM pass (runsk.hip, u32, lk = 1..4): src holds
 // ascending runs of 2^lw keys, dst gets ascending runs of 2^(lw+lk) (2^lk-way
 // merge of each group of runs; the last group may be short).  Chunks are cut
-// at fences (every 256th key of a run): `phase` selects which of two
+// at fences (every 128th key of a run): `phase` selects which of two
 // per-stream fence buffers holds this pass's fences; gather = build them from
 // src first (the pass after a non-multi-way pass); lk_next > 0 = write the
 // fences of the next multi-way pass (runs of 2^(lw+lk), groups of 2^lk_next)

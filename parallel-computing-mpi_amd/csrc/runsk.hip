@@ -1,8 +1,9 @@
 // runsk.hip -- K-way merge passes of the local sort (gfx950, u32 keys):
-// ascending runs of W = 2^lw keys, in groups of K = 2^lk (lk = 1, 2, 3), ->
+// ascending runs of W = 2^lw keys, in groups of K = 2^lk (lk = 1..4), ->
 // ascending runs of K*W.  One HBM read + one HBM write per key for lk merge
 // levels (runs.hip does one level per pass): 2^30 keys past the 2^15-key SORT
-// tile take five 8-way passes instead of fifteen 2-way ones.
+// tile take five 8-way passes instead of fifteen 2-way ones (16-way passes are
+// built too: MISORT_MULTIWAY=4).
 //
 // The reference's local sort is std::sort (psort.cc:175); any correct sort of
 // payload-free keys writes the same bytes, so the levels past the bitonic SORT
@@ -42,7 +43,10 @@
 namespace misort {
 namespace {
 
-constexpr int FG_LOG2 = 8;
+#ifndef MISORT_MK_FG_LOG2
+#define MISORT_MK_FG_LOG2 7
+#endif
+constexpr int FG_LOG2 = MISORT_MK_FG_LOG2;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
 constexpr int CAP = 8192;                       // most keys of a chunk
 #ifndef MISORT_MK_NT
@@ -63,8 +67,8 @@ constexpr int WG_PER_CU = 4;
 template <int LK>
 struct Shape {
     static constexpr int K = 1 << LK;
-    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk: 30 / 28 / 24
-    static constexpr int RW = LK == 3 ? 128 : 256;  // load row: RW keys of one segment
+    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk: 62 / 60 / 56 / 48
+    static constexpr int RW = LK == 4 ? 64 : LK == 3 ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_WORDS = PAD + CAP + K * (G + IT) + 16;
@@ -127,16 +131,16 @@ __global__ void k_fence_gather(const uint32_t* __restrict__ src, int64_t n, int 
     F[i] = fpack(src[gp], gp, lw, lk);
 }
 
-// The fences of one group (<= 8192) merged into total order in LDS: each
-// fence's rank = its index in its run's list + its lower bound in the others.
+// Runs of 2^wf fences merged 2^a at a time (<= 8192 fences) into total order
+// in LDS: block b takes fences [b << (wf + a), ...); each fence's rank = its
+// index in its run's list + its lower bound in the sub-group's other runs.
 __global__ __launch_bounds__(1024) void k_fence_lds(const uint64_t* __restrict__ F, uint64_t* __restrict__ M,
-                                                    Geo geo) {
+                                                    int64_t nf, int wf_log2, int a) {
     extern __shared__ uint64_t sf[];
-    const int64_t g = blockIdx.x;
-    const int64_t f0 = geo.base(g) >> FG_LOG2;
-    const int nfg = (int)geo.nfences(g);
-    const int wf = (int)(geo.W() >> FG_LOG2);  // fences per full run
-    const int K = geo.K();
+    const int64_t f0 = (int64_t)blockIdx.x << (wf_log2 + a);
+    const int nfg = (int)((nf - f0) < ((int64_t)1 << (wf_log2 + a)) ? nf - f0 : ((int64_t)1 << (wf_log2 + a)));
+    const int wf = 1 << wf_log2;
+    const int K = 1 << a;
     for (int e = threadIdx.x; e < nfg; e += blockDim.x) sf[e] = F[f0 + e];
     __syncthreads();
     for (int e = threadIdx.x; e < nfg; e += blockDim.x) {
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const uint64_t* __rest
     __shared__ int sw[SCAN_NT / 64];
     const int64_t c = (int64_t)blockIdx.x * SCAN_NT + threadIdx.x;
     const int K = geo.K();
-    int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int cnt[16] = {};
     if (c < nchunks) {
         int64_t g, t;
         chunk_place(geo, c, g, t);
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const uint64_t* __rest
         for (int64_t e = e0; e < e1; ++e) {
             const int r = (int)((m[e] >> (32 - geo.lk)) & (K - 1));
 #pragma unroll
-            for (int q = 0; q < 8; ++q) cnt[q] += q == r;
+            for (int q = 0; q < 16; ++q) cnt[q] += q == r;
         }
     }
     for (int q = 0; q < K; ++q) {
@@ -241,9 +245,9 @@ __global__ __launch_bounds__(SCAN_NT) void k_scan_totals(int* __restrict__ bsum,
 // (a position within the run), or the run's length for the group's end slot.
 // Run r's fences before the chunk-start fence f come from the scanned counts;
 // the keys before f lie among the FG positions after the last of them.
-__global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __restrict__ M,
-                         const int* __restrict__ P, const int* __restrict__ bsum, Geo geo, int64_t nslots,
-                         int64_t* __restrict__ bounds) {
+__global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __restrict__ F,
+                         const uint64_t* __restrict__ M, const int* __restrict__ P, const int* __restrict__ bsum,
+                         Geo geo, int64_t nslots, int64_t* __restrict__ bounds) {
     const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= (nslots << geo.lk)) return;
     const int64_t s = id >> geo.lk;
@@ -281,19 +285,66 @@ __global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __res
         bounds[id] = 0;
         return;
     }
-    // keys before f: all of positions <= (lo-1)*FG, none from lo*FG on (a
-    // binary search: 8 dependent loads within one 1 KiB window measured 4x
-    // faster than two rounds of 16 independent ones -- the pass is bound by
-    // the load count, not by their latency)
-    const uint32_t* kr = src + base + r * W;
-    int64_t a = ((lo - 1) << FG_LOG2) + 1, b = (lo << FG_LOG2) < len ? (lo << FG_LOG2) : len;
-    while (a < b) {  // first position after f: key > v (r < r0) or key >= v (r > r0)
-        const int64_t mid = (a + b) >> 1;
-        const uint32_t k = kr[mid];
-        if (r < r0 ? k <= v : k < v) a = mid + 1;
-        else b = mid;
+    if (lo > (len + FG - 1) >> FG_LOG2) {  // more fences than the run has: malformed input fences
+        bounds[id] = -1;                    // k_chunk_desc rejects the chunk; no read outside the run
+        return;
     }
-    bounds[id] = a;
+    // keys before f: all of positions <= (lo-1)*FG, none from lo*FG on.  The
+    // first position after f (key > v if r < r0, key >= v if r > r0) lies in
+    // [a, b]; it is guessed by interpolating v between the window's two
+    // fence keys, bracketed by galloping from the guess, then binary-searched:
+    // on spread keys the probes stay within a line or two of the answer
+    // (a plain binary search touches ~5 lines of the 1 KiB window; the kernel
+    // is bound by those probe lines).
+    const uint32_t* kr = src + base + r * W;
+    const uint64_t* fr = F + ((base + r * W) >> FG_LOG2);
+    const int64_t a = ((lo - 1) << FG_LOG2) + 1, b = (lo << FG_LOG2) < len ? (lo << FG_LOG2) : len;
+    const bool le = r < r0;
+    auto before = [&](int64_t q) {
+        const uint32_t k = kr[q];
+        return le ? k <= v : k < v;
+    };
+    const uint32_t ka = (uint32_t)(fr[lo - 1] >> 32);
+    int64_t p = a + ((b - a) >> 1);
+    if ((lo << FG_LOG2) < len) {
+        const uint32_t kb = (uint32_t)(fr[lo] >> 32);
+        if (kb > ka) p = a + (int64_t)(((uint64_t)(v - ka) * (uint64_t)(b - a)) / (uint64_t)(kb - ka));
+    }
+    p = p < a ? a : (p > b ? b : p);
+    int64_t lo_b, hi_b;  // the answer lies in [lo_b, hi_b]
+    if (p < b && before(p)) {
+        lo_b = p + 1;
+        hi_b = b;
+        for (int64_t step = 4;; step <<= 1) {
+            const int64_t x = lo_b + step - 1;
+            if (x >= hi_b) break;
+            if (before(x)) {
+                lo_b = x + 1;
+            } else {
+                hi_b = x;
+                break;
+            }
+        }
+    } else {
+        lo_b = a;
+        hi_b = p;
+        for (int64_t step = 4;; step <<= 1) {
+            const int64_t x = hi_b - step;
+            if (x < lo_b) break;
+            if (!before(x)) {
+                hi_b = x;
+            } else {
+                lo_b = x + 1;
+                break;
+            }
+        }
+    }
+    while (lo_b < hi_b) {
+        const int64_t mid = (lo_b + hi_b) >> 1;
+        if (before(mid)) lo_b = mid + 1;
+        else hi_b = mid;
+    }
+    bounds[id] = lo_b;
 }
 
 // Chunk descriptors: for chunk c, its group's base, its output offset, the
@@ -309,97 +360,121 @@ __global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __res
 // a bad chunk gets no rows and is left unwritten (the sort then fails its
 // checks).
 template <int LK>
-struct Desc {
+struct alignas(128) Desc {  // whole 128-byte lines: a chunk's entries never share a line with another's
     int64_t gbase, out0;
     int o[Shape<LK>::K + 1];           // chunk position of segment r; o[K] = chunk length
     uint32_t off[Shape<LK>::NROWS];  // byte offset of the row's first key from the group base
     uint32_t la[Shape<LK>::NROWS];   // real keys of the row (0..RW) | LDS word of its first key << 16
 };
 
-// One wave per chunk (DESC_CPB chunks per workgroup): K lanes read and check
-// the chunk's bounds, every lane gets them by shuffles, then the lanes write
-// the table entries.
-constexpr int DESC_CPB = 4;
+// One wave per DESC_CPW consecutive chunks (DESC_CPB waves per workgroup):
+// K lanes read and check each chunk's bounds -- all the wave's bounds loads
+// first, then the chunks one by one -- every lane gets them by shuffles, then
+// the lanes write the table entries.
+constexpr int DESC_CPB = 4, DESC_CPW = 4;
+
 template <int LK>
-__global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo,
-                                                             int64_t nchunks, Desc<LK>* __restrict__ desc) {
+__device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, int lane, int64_t st, int64_t en,
+                                         Desc<LK>* __restrict__ desc) {
     typedef Shape<LK> S;
     constexpr int K = S::K;
-    const int64_t c = (int64_t)blockIdx.x * DESC_CPB + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (c >= nchunks) return;  // whole waves
-    int64_t g, t;
-    chunk_place(geo, c, g, t);
-    const int64_t* b0 = bounds + K * geo.slot(g, t);
-    int64_t st = 0, ln = 0;
+    const int64_t ln = en - st;
     bool ok = true;
-    if (lane < K) {
-        st = b0[lane];
-        ln = b0[K + lane] - st;
-        ok = st >= 0 && ln >= 0 && st + ln <= geo.run_len(g, lane) && ln <= CAP;
-    }
+    if (lane < K) ok = st >= 0 && ln >= 0 && en <= geo.run_len(g, lane) && ln <= CAP;
     // bounds outside the runs would be a logic error: never let them address memory
     ok = __all(ok);
-    int sln[K], srow[K + 1], so[K + 1];
-    int64_t out = geo.base(g);
+    // the K lanes' values as scalars (starts < W <= 2^27 and lengths <= CAP fit 32 bits)
+    int sln[K], sst[K];
     int tot = 0;
 #pragma unroll
     for (int r = 0; r < K; ++r) {
-        sln[r] = __shfl((int)ln, r, 64);
+        sln[r] = __builtin_amdgcn_readlane((int)ln, r);
+        sst[r] = __builtin_amdgcn_readlane((int)st, r);
         tot += sln[r];
     }
     ok = ok && tot <= CAP;
+    int srow[K + 1], so[K + 1];
+    uint32_t sb[K];  // byte offset of segment r's first key from the group base (< KW*4 <= 2^32)
     int R = 0, o = 0;
+    int64_t out = geo.base(g);
 #pragma unroll
     for (int r = 0; r < K; ++r) {
-        if (!ok) sln[r] = 0;
+        if (!ok) sln[r] = sst[r] = 0;
         srow[r] = R;
         so[r] = o;
+        sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)sst[r]) * 4u;
         R += (sln[r] + S::RW - 1) / S::RW;
         o += sln[r];
+        out += sst[r];
     }
     srow[K] = R;
     so[K] = o;
-    const int64_t stl = ok ? st : 0;
     Desc<LK>& d = desc[c];
-    int64_t sum = stl;  // out0 = group base + sum of the segment starts
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m, 64);
     if (lane == 0) {
         d.gbase = geo.base(g);
-        d.out0 = out + sum;
+        d.out0 = out;
     }
 #pragma unroll
     for (int r = 0; r <= K; ++r)
         if (lane == r) d.o[r] = so[r];
-    int64_t sst[K];
-#pragma unroll
-    for (int r = 0; r < K; ++r) sst[r] = __shfl(stl, r, 64);  // all lanes active
     for (int j = lane; j < S::NROWS; j += 64) {
         const int row = (j % IT) * S::NR + j / IT;  // table entry j (stored by part)
-        uint32_t off = 0, la = 0;                   // rows past the chunk: no keys
+        // the row's segment: the last one starting at or before it
+        int rr = 0;
+#pragma unroll
+        for (int r = 1; r < K; ++r) rr = row >= srow[r] ? r : rr;
+        int rs = 0, rl = 0, rb = 0;
+        uint32_t ro = 0;
 #pragma unroll
         for (int r = 0; r < K; ++r) {
-            if (row >= srow[r] && row < srow[r + 1]) {
-                const int k = row - srow[r];
-                const int rem = sln[r] - k * S::RW;
-                off = (uint32_t)((((int64_t)r << geo.lw) + sst[r] + (int64_t)k * S::RW) * 4);  // < KW*4 <= 2^32
-                la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(so[r] + r * G + k * S::RW) << 16);
+            if (rr == r) {
+                rs = srow[r];
+                rl = sln[r];
+                rb = so[r] + r * G;
+                ro = sb[r];
             }
         }
-        d.off[j] = off;
-        d.la[j] = la;
+        const int k = row - rs, rem = rl - k * S::RW;
+        const bool in = row < srow[K];  // rows past the chunk: no keys
+        d.off[j] = in ? ro + (uint32_t)(k * S::RW * 4) : 0u;
+        d.la[j] = in ? (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(rb + k * S::RW) << 16) : 0u;
     }
+}
+
+template <int LK>
+__global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo,
+                                                             int64_t nchunks, Desc<LK>* __restrict__ desc) {
+    constexpr int K = Shape<LK>::K;
+    const int64_t c0 = ((int64_t)blockIdx.x * DESC_CPB + (threadIdx.x >> 6)) * DESC_CPW;
+    const int lane = threadIdx.x & 63;
+    int64_t g[DESC_CPW], st[DESC_CPW], en[DESC_CPW];
+#pragma unroll
+    for (int i = 0; i < DESC_CPW; ++i) {
+        st[i] = en[i] = g[i] = 0;
+        if (c0 + i < nchunks) {  // whole waves
+            int64_t t;
+            chunk_place(geo, c0 + i, g[i], t);
+            const int64_t* b0 = bounds + K * geo.slot(g[i], t);
+            if (lane < K) {
+                st[i] = b0[lane];
+                en[i] = b0[K + lane];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < DESC_CPW; ++i)
+        if (c0 + i < nchunks) desc_one<LK>(geo, c0 + i, g[i], lane, st[i], en[i], desc);
 }
 
 // Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
 // (every A key before it <= every B key after it and vice versa; any such
 // split gives the same output values -- the keys carry no payload).  The
 // largest base in [lo, hi] with A[i - 1] <= B[d - i] for every i <= base, by
-// 13 power-of-two steps (hi - lo <= min(LA, LB) <= CAP/2 = 2^12) with clamped
-// probes: no loop control, no branches.  Probe addresses stay inside
-// [A0 - 1, A0 + LA) and [B0, B0 + LB].
-__device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d) {
+// power-of-two steps with clamped probes, no data-dependent branches: the
+// steps 2^j <= maxr, a uniform bound on hi - lo <= min(LA, LB) (<= CAP/2 =
+// 2^12), sum to >= hi - lo.  Probe addresses stay inside [A0 - 1, A0 + LA)
+// and [B0, B0 + LB].
+__device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d, int maxr) {
     static_assert(CAP / 2 <= 8191, "co-rank steps");
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
@@ -408,6 +483,7 @@ __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0
     int base = lo;
 #pragma unroll
     for (int step = 4096; step >= 1; step >>= 1) {
+        if (step > maxr) continue;  // uniform
         const int i = base + step;
         const int ic = i < hi ? i : hi;
         const bool ok = i <= hi && a[ic] <= b[-ic];
@@ -423,11 +499,11 @@ __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0
 // (swapping the two read pointers when that side changes) -- six VALU ops and
 // one LDS read per output.  Ties may go either way: equal keys are identical.
 // Past the end of both sequences a chain outputs MAX (their sentinels).
-__device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d,
+__device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d, int maxr,
                                             uint32_t (&r)[IT]) {
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
-    const int ia = co_rank(s, A0, LA, B0, LB, dc);
+    const int ia = co_rank(s, A0, LA, B0, LB, dc, maxr);
     // byte addresses of the two heads (LDS pointers are 32-bit)
     uint32_t px = lds_addr(s + A0 + ia), py = lds_addr(s + B0 + dc - ia);
     uint32_t h = lds_ld(px), g = lds_ld(py);
@@ -507,9 +583,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
         // pair p's output: [qp[p], qp[p] + lp[p]), then G sentinels; the next
         // pair starts at the first lane boundary past them
         int qp[K / 2], lp[K / 2];
-        int qa = 0;
+        int qa = 0, maxr = 0;  // maxr: the longest co-rank range of the level's pairs (uniform)
 #pragma unroll
         for (int p = 0; p < P; ++p) {
+            const int mr = ln[2 * p] < ln[2 * p + 1] ? ln[2 * p] : ln[2 * p + 1];
+            maxr = mr > maxr ? mr : maxr;
             lp[p] = ln[2 * p] + ln[2 * p + 1];
             qp[p] = qa;
             qa = (qa + lp[p] + G + IT - 1) / IT * IT;
@@ -531,7 +609,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            merge_chain(s, A0, LA, B0, LB, pos - Q, r);
+            merge_chain(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         __syncthreads();
         if (lv < LK) {
@@ -597,13 +675,16 @@ struct Scratch {
     size_t bytes = 0;
 };
 std::mutex g_mu;
-std::map<std::pair<int, hipStream_t>, Scratch> g_scr;
+std::map<std::pair<int, hipStream_t>, Scratch> g_scr[2];
 
-void* scratch(size_t bytes, hipStream_t s) {
+// which = 0: the two fence buffers (a pass's input fences are the previous
+// pass's output: sized by n alone, so they never move between the passes of
+// one sort); which = 1: per-pass planning data (free to grow at any pass).
+void* scratch(int which, size_t bytes, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(g_mu);
-    auto& e = g_scr[{dev, s}];
+    auto& e = g_scr[which][{dev, s}];
     if (e.bytes < bytes) {
         if (e.p && (hipStreamSynchronize(s) != hipSuccess || hipFree(e.p) != hipSuccess)) return nullptr;
         e = Scratch{};
@@ -629,45 +710,54 @@ hipError_t merge_pass(const uint32_t* src, uint32_t* dst, int64_t n, int lw, hip
     const int64_t nslots = geo.nfull * (geo.kf + 1) + (tail ? geo.nchunks(geo.nfull) + 1 : 0);
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
     if (nchunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-    // layout: fence buffers 0 and 1, merged fences, u64 merge temp, bounds,
-    // fence counts and their block totals, descriptors
+    // fence buffers 0 and 1 (kept across passes); per pass: merged fences,
+    // u64 merge temp, bounds, fence counts and their block totals, descriptors
     const int64_t nbk = (nchunks + SCAN_NT - 1) / SCAN_NT;
     const size_t fb = ((size_t)nf * 8 + 255) & ~(size_t)255;
     const size_t bb = ((size_t)nslots * S::K * 8 + 255) & ~(size_t)255;
     const size_t cb = ((size_t)nbk * SCAN_NT * S::K * 4 + 255) & ~(size_t)255;
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
-    char* base = (char*)scratch(4 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<LK>) + 256, s);
-    if (!base) return hipErrorOutOfMemory;
-    int* cnt = (int*)(base + 4 * fb + bb);
-    int* bsum = (int*)(base + 4 * fb + bb + cb);
-    uint64_t* F = (uint64_t*)(base + (phase & 1) * fb);
-    uint64_t* Fn = (uint64_t*)(base + ((phase & 1) ^ 1) * fb);
-    uint64_t* M = (uint64_t*)(base + 2 * fb);
-    uint64_t* T = (uint64_t*)(base + 3 * fb);
-    int64_t* bounds = (int64_t*)(base + 4 * fb);
-    Desc<LK>* desc = (Desc<LK>*)(base + 4 * fb + bb + cb + sb);
+    char* fbase = (char*)scratch(0, 2 * fb, s);
+    char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<LK>) + 256, s);
+    if (!base || !fbase) return hipErrorOutOfMemory;
+    uint64_t* F = (uint64_t*)(fbase + (phase & 1) * fb);
+    uint64_t* Fn = (uint64_t*)(fbase + ((phase & 1) ^ 1) * fb);
+    uint64_t* M = (uint64_t*)base;
+    uint64_t* T = (uint64_t*)(base + fb);
+    int64_t* bounds = (int64_t*)(base + 2 * fb);
+    int* cnt = (int*)(base + 2 * fb + bb);
+    int* bsum = (int*)(base + 2 * fb + bb + cb);
+    Desc<LK>* desc = (Desc<LK>*)(base + 2 * fb + bb + cb + sb);
     if (gather) k_fence_gather<<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
     const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
-    if (wf_log2 + LK <= 13) {          // group fences <= 8192: 64 KiB of LDS
-        const int ngroups = (int)(geo.nfull + (tail ? 1 : 0));
-        const size_t lds = ((size_t)1 << (wf_log2 + LK)) * 8;
-        k_fence_lds<<<ngroups, 1024, lds, s>>>(F, M, geo);
-    } else {
-        // LK u64 merge levels landing in M: F -> M; F -> T -> M; F -> M -> T -> M
-        const uint64_t* a = F;
-        for (int l = 0; l < LK; ++l) {
-            uint64_t* b = ((LK - 1 - l) & 1) ? T : M;
-            const hipError_t e = merge_level<uint64_t>(a, b, nf, wf_log2 + l, s);
+    {
+        // the group's fences into total order, landing in M: the first a levels
+        // in LDS (sub-groups of 2^a runs, <= 8192 fences = 64 KiB), the other
+        // LK - a as u64 merge levels (runs of >= 2^13 fences), ping-ponging
+        // through T
+        const int a = wf_log2 >= 13 ? 0 : (13 - wf_log2 < LK ? 13 - wf_log2 : LK);
+        const uint64_t* x = F;
+        int left = LK - a;
+        if (a > 0) {
+            uint64_t* y = (left & 1) ? T : M;
+            const size_t lds = ((size_t)1 << (wf_log2 + a)) * 8;
+            const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
+            k_fence_lds<<<(unsigned)nb0, 1024, lds, s>>>(F, y, nf, wf_log2, a);
+            x = y;
+        }
+        for (int l = a; l < LK; ++l, --left) {
+            uint64_t* y = ((left - 1) & 1) ? T : M;
+            const hipError_t e = merge_level<uint64_t>(x, y, nf, wf_log2 + l, s);
             if (e != hipSuccess) return e;
-            a = b;
+            x = y;
         }
     }
     const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
     k_fence_counts<<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
-    k_bounds<<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, M, cnt, bsum, geo, nslots, bounds);
-    k_chunk_desc<LK><<<(unsigned)((nchunks + DESC_CPB - 1) / DESC_CPB), 64 * DESC_CPB, 0, s>>>(bounds, geo, nchunks,
-                                                                                             desc);
+    k_bounds<<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots, bounds);
+    k_chunk_desc<LK><<<(unsigned)((nchunks + DESC_CPB * DESC_CPW - 1) / (DESC_CPB * DESC_CPW)), 64 * DESC_CPB, 0, s>>>(
+        bounds, geo, nchunks, desc);
     const unsigned grid = (unsigned)nchunks;
     if (lk_next > 0) k_mergek<LK, true><<<grid, NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
     else k_mergek<LK, false><<<grid, NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
@@ -701,11 +791,12 @@ hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, i
     if (n <= 0) return hipSuccess;
     // load rows address a group with 32-bit byte offsets (KW*4 <= 2^32); runs
     // at least a 2^15 SORT tile long
-    if (lk < 1 || lk > 3 || lw < 15 || lw + lk > 30 || src == dst || lk_next < 0 || lk_next > 3)
+    if (lk < 1 || lk > 4 || lw < 15 || lw + lk > 30 || src == dst || lk_next < 0 || lk_next > 4)
         return hipErrorInvalidValue;
     if (lk == 1) return merge_pass<1>(src, dst, n, lw, s, phase, gather, lk_next);
     if (lk == 2) return merge_pass<2>(src, dst, n, lw, s, phase, gather, lk_next);
-    return merge_pass<3>(src, dst, n, lw, s, phase, gather, lk_next);
+    if (lk == 3) return merge_pass<3>(src, dst, n, lw, s, phase, gather, lk_next);
+    return merge_pass<4>(src, dst, n, lw, s, phase, gather, lk_next);
 }
 
 }  // namespace misort

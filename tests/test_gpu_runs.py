@@ -1,7 +1,7 @@
 """GPU parity of the merge levels (runs.hip) -- the passes that finish the
 local sort replacing the reference's std::sort (psort.cc:175) once runs leave
 the SORT tile: 2-way levels (runs.hip) and 2^lk-way passes of lk levels each
-(runsk.hip, lk = 1..3).
+(runsk.hip, lk = 1..4).
 
 * One merge level (misort_pass_probe, kind run_merge) on inputs made of
   ascending runs of 2^hi keys, ragged tails included, is compared bit for bit
@@ -96,7 +96,7 @@ def test_merge_level_duplicates_and_single_run(ctx, dt):
         np.testing.assert_array_equal(run_level(ctx, x, hi), expect(x, hi))
 
 
-@pytest.mark.parametrize("lk", [1, 2, 3])
+@pytest.mark.parametrize("lk", [1, 2, 3, 4])
 @pytest.mark.parametrize("hi", [15, 16, 17])
 @pytest.mark.parametrize("n", [(1 << 20) + 3, (1 << 19), (1 << 19) - 4097, 3 * (1 << 17) + 5, 5000, 12345, 2049])
 def test_mergek_level_matches_numpy(ctx, lk, hi, n):
@@ -106,7 +106,7 @@ def test_mergek_level_matches_numpy(ctx, lk, hi, n):
     np.testing.assert_array_equal(run_level(ctx, x, hi, "run_mergek", lk), expectk(x, hi, lk))
 
 
-@pytest.mark.parametrize("lk", [1, 2, 3])
+@pytest.mark.parametrize("lk", [1, 2, 3, 4])
 @pytest.mark.parametrize("hi", [15, 16, 21])
 def test_mergek_level_ties_and_edges(ctx, lk, hi):
     """Duplicate-heavy, all-equal (every fence the same key: chunks cut by
@@ -132,7 +132,7 @@ def test_merge_level_rejects_bad_shapes(ctx):
     for hi in (5, 11):  # runs shorter than the merge tile
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi)
-    for hi, lk in ((11, 2), (14, 2), (15, 4)):  # multi-way: runs shorter than a SORT tile; lk > 3
+    for hi, lk in ((11, 2), (14, 2), (15, 5)):  # multi-way: runs shorter than a SORT tile; lk > 4
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi, "run_mergek", lk)
 
@@ -181,6 +181,7 @@ ctx.close()
     (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
     (4, {"MISORT_MERGE_FROM": "15"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
     (4, {"MISORT_MERGE_FROM": "15"}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
+    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "4"}, (1 << 25) + 3),  # 4 + 3 + 3 levels (16-way)
     (4, {"MISORT_MERGE_FROM": "15"}, 3 * (1 << 23) + 5),
     (4, {"MISORT_MERGE_FROM": "15"}, (1 << 17) + 1),
     (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),

@@ -8,11 +8,11 @@ independently.  Checks the properties the kernels rely on: chunks tile each
 group exactly, no chunk exceeds CAP keys nor the load rows (RW keys of one
 segment, NROWS per chunk), every chunk's keys precede the next chunk's, and
 the chunk/slot indexing (chunks per full group = ceil(fences / FM)) matches
-the bounds layout.  K = 2^lk, lk = 1, 2, 3."""
+the bounds layout.  K = 2^lk, lk = 1..4."""
 import numpy as np
 import pytest
 
-FG_LOG2, CAP = 8, 8192
+FG_LOG2, CAP = 7, 8192
 NT, IT = 512, 18  # k_mergek lanes and keys per lane
 FG = 1 << FG_LOG2
 
@@ -20,7 +20,7 @@ FG = 1 << FG_LOG2
 def shape(lk):
     """(K, FM, RW, NROWS) of runsk.hip's Shape<lk>."""
     K = 1 << lk
-    rw = 128 if lk == 3 else 256
+    rw = 64 if lk == 4 else 128 if lk == 3 else 256
     return K, CAP // FG - K, rw, IT * NT // rw
 
 
@@ -58,25 +58,56 @@ def chunk_bounds(x, lw, lk, g, F):
             # FG positions between two of them
             fr = F[(base + r * W) >> FG_LOG2: ((base + r * W) >> FG_LOG2) + ((lens[r] + FG - 1) >> FG_LOG2)]
             lo = int(np.searchsorted(fr, np.uint64(f), side="left"))
-            if lo == 0:
-                got = 0
-            else:
-                a, b = ((lo - 1) << FG_LOG2) + 1, min(lo << FG_LOG2, lens[r])
-                while a < b:
-                    mid = (a + b) >> 1
-                    before = run[mid] <= v if r < r0 else run[mid] < v
-                    if before:
-                        a = mid + 1
-                    else:
-                        b = mid
-                got = a
+            got = 0 if lo == 0 else refine(run, fr, lo, lens[r], v, r < r0)
             assert got == want
         out.append(st)
     out.append(lens)
     return out, lens
 
 
-@pytest.mark.parametrize("lk", [1, 2, 3])
+def refine(run, fr, lo, ln, v, le):
+    """k_bounds' window search: the first position in [a, b] whose key is not
+    before the fence (key > v if le, key >= v otherwise), guessed by
+    interpolating v between the window's fence keys, bracketed by galloping
+    from the guess, then binary-searched."""
+    def before(q):
+        return run[q] <= v if le else run[q] < v
+    a, b = ((lo - 1) << FG_LOG2) + 1, min(lo << FG_LOG2, ln)
+    ka = int(fr[lo - 1]) >> 32
+    p = a + ((b - a) >> 1)
+    if (lo << FG_LOG2) < ln:
+        kb = int(fr[lo]) >> 32
+        if kb > ka:
+            p = a + ((v - ka) * (b - a)) // (kb - ka)
+    p = min(max(p, a), b)
+    if p < b and before(p):
+        lo_b, hi_b, step = p + 1, b, 4
+        while lo_b + step - 1 < hi_b:
+            x = lo_b + step - 1
+            if before(x):
+                lo_b, step = x + 1, step * 2
+            else:
+                hi_b = x
+                break
+    else:
+        lo_b, hi_b, step = a, p, 4
+        while hi_b - step >= lo_b:
+            x = hi_b - step
+            if not before(x):
+                hi_b, step = x, step * 2
+            else:
+                lo_b = x + 1
+                break
+    while lo_b < hi_b:
+        mid = (lo_b + hi_b) >> 1
+        if before(mid):
+            lo_b = mid + 1
+        else:
+            hi_b = mid
+    return lo_b
+
+
+@pytest.mark.parametrize("lk", [1, 2, 3, 4])
 @pytest.mark.parametrize("lw", [15, 16])
 @pytest.mark.parametrize("n_groups,tail", [(2, 0), (1, 3 * (1 << 15) + 5), (1, 777), (0, (1 << 15) * 2 + 1)])
 @pytest.mark.parametrize("kind", ["uniform", "dup", "equal", "interleaved"])

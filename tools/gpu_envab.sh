@@ -1,8 +1,18 @@
-# Env A/B of bench.py: each line of $CASES is "<label>|<env assignments>|<bench args>".
+# A/B of (library, env) combinations on the bench: RUNS="name|lib|ENV=V ENV2=V2" entries separated by ';'.
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out/envab
-echo "$CASES" | while IFS='|' read -r lab envs args; do
-  [ -z "$lab" ] && continue
-  env $envs timeout -k 10 200 python -u bench.py $args --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/envab/$lab.log 2>&1 || { echo "FAIL $lab"; tail -5 gpurun_out/envab/$lab.log; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/envab/$lab.log').read().strip().splitlines()[-1]); print('$lab', round(d['value'],2), 'Gkeys/s', round(d['ms_per_step'],2), 'ms err', d['check_errors'], {k:(v['launches_per_step'], round(v['avg_launch_us'])) for k,v in d['kernels'].items()})" || exit 1
+R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${OUTDIR:-envab}"; mkdir -p "$O"; cd "$R"
+IFS=';' read -ra specs <<< "$RUNS"
+for rep in 1 2; do
+for spec in "${specs[@]}"; do
+  IFS='|' read -r name lib envs <<< "$spec"
+  if [ -n "$lib" ]; then export MISORT_LIBRARY="$R/$lib"; else unset MISORT_LIBRARY; fi
+  env $envs timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps ${STEPS:-10} $BENCH_ARGS > "$O/bench_${name}_$rep.json" 2> "$O/bench_${name}_$rep.err"; rc=$?
+  case $rc in 124|137|134|139) echo "fatal rc $rc in $name"; exit $rc;; esac
+  [ $rc -ne 0 ] && { echo "$name rc $rc"; tail -3 "$O/bench_${name}_$rep.err"; continue; }
+  python3 -c "
+import json; d=json.loads(open('$O/bench_${name}_$rep.json').read().strip().splitlines()[-1])
+print('$name', $rep, round(d['value'],2), 'Gkeys/s', round(d['ms_per_step'],2), 'ms err', d['check_errors'], ' '.join(f'{k}:{v[\"launches_per_step\"]:.0f}x{v[\"avg_launch_us\"]:.0f}us' for k,v in d.get('kernels',{}).items()))"
 done
+done
+unset MISORT_LIBRARY
+exit 0
