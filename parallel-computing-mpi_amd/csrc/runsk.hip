@@ -53,8 +53,8 @@ constexpr int CAP = 8192;                       // most keys of a chunk
 #define MISORT_MK_NT 512
 #endif
 constexpr int NT = MISORT_MK_NT;         // lanes per chunk workgroup
-constexpr int IT = NT == 256 ? 36 : 18;  // keys per lane
-static_assert(NT == 256 || NT == 512, "chunk workgroup");
+constexpr int IT = 9216 / NT;            // keys per lane (NT * IT = 9216 slots for CAP = 8192 plus layout gaps)
+static_assert(NT == 256 || NT == 384 || NT == 512, "chunk workgroup");
 // Every sequence an in-LDS merge reads is followed by G words of MAX
 // (sentinels), so a merge chain needs no end checks: it reads at most IT words
 // past an exhausted sequence.  Each level places its pairs' outputs at lane
@@ -68,7 +68,7 @@ template <int LK>
 struct Shape {
     static constexpr int K = 1 << LK;
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk: 62 / 60 / 56 / 48
-    static constexpr int RW = LK == 4 ? 64 : LK == 3 ? 128 : 256;  // load row: RW keys of one segment
+    static constexpr int RW = LK == 4 ? 64 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_WORDS = PAD + CAP + K * (G + IT) + 16;

@@ -176,6 +176,9 @@ struct Transport {
     // all ranks' int64 value, host-visible on return
     virtual int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all,
                               hipStream_t s) = 0;
+    // the same from `count` int64 values already in device memory (d_mine),
+    // so a size computed on the device needs no host round trip before it
+    virtual int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) = 0;
     // device buffers; both sides know both byte counts
     virtual int sendrecv(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, int peer,
                          hipStream_t s) = 0;
@@ -208,6 +211,16 @@ struct RcclTransport final : Transport {
         HIPCHK(hipMemcpyAsync(d + (size_t)count * nranks, mine, sizeof(int64_t) * count,
                               hipMemcpyHostToDevice, s));
         NCCLCHK(ncclAllGather(d + (size_t)count * nranks, d, count, ncclInt64, comm, s));
+        all.resize((size_t)count * nranks);
+        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return MISORT_OK;
+    }
+    int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
+        int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
+        if (rc) return rc;
+        int64_t* d = (int64_t*)buf.p;
+        NCCLCHK(ncclAllGather(d_mine, d, count, ncclInt64, comm, s));
         all.resize((size_t)count * nranks);
         HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -298,6 +311,12 @@ struct LocalTransport final : Transport {
         if (me.ready) (void)hipEventDestroy(me.ready);
         if (me.done) (void)hipEventDestroy(me.done);
         me.ready = me.done = nullptr;
+    }
+    int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
+        std::vector<int64_t> mine((size_t)count);
+        HIPCHK(hipMemcpyAsync(mine.data(), d_mine, sizeof(int64_t) * count, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return allgather_i64(mine.data(), count, all, s);
     }
     int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t) override {
         {
@@ -515,12 +534,14 @@ int64_t corank_lower(const std::vector<T>& sa, int64_t na, const std::vector<T>&
 // direct time (4x less at P = 8).  All ranks take part, including those whose
 // own message is empty, because they relay for the others.
 int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sbytes, void* rbuf, size_t rbytes,
-                   hipStream_t s, size_t* rbytes_out = nullptr) {
+                   hipStream_t s, size_t* rbytes_out = nullptr, const std::vector<int64_t>* known = nullptr) {
     const int P = c->nranks, me = c->rank, pm = me ^ (1 << bit);
     int rc;
     std::vector<int64_t> m;  // units (w bytes) each rank sends to its partner
     const int64_t mine = (int64_t)(sbytes / w);
-    if ((rc = c->tr->allgather_i64(&mine, 1, m, s))) return rc;
+    if (known) m = *known;  // gathered by the caller
+    else if ((rc = c->tr->allgather_i64(&mine, 1, m, s))) return rc;
+    if ((int)m.size() != P || m[me] != mine) return fail(MISORT_E_INVALID, "relay: size table mismatch");
     if (rbytes_out) {  // the partner's size is learnt here; rbytes is the capacity
         if ((size_t)m[pm] * w > rbytes) return fail(MISORT_E_CAPACITY, "relay: partner message exceeds buffer");
         *rbytes_out = (size_t)m[pm] * w;
@@ -574,6 +595,33 @@ int relay_exchange(misort_ctx* c, size_t w, int bit, const void* sbuf, size_t sb
     return c->tr->group_p2p(r2, s);
 }
 
+// The message sizes of a relayed stage: every rank contributes the pair
+// (coded words, raw words) from device memory (d_pair, 2 int64) and sends
+// min of the two; all ranks of the stage make this same collective call,
+// whatever their own message is (coded, raw or empty).  units[r] = rank r's
+// message in 4-byte words.
+int relay_sizes(misort_ctx* c, const int64_t* d_pair, std::vector<int64_t>& pairs, std::vector<int64_t>& units,
+                hipStream_t s) {
+    int rc = c->tr->allgather_i64_dev(d_pair, 2, pairs, s);
+    if (rc) return rc;
+    units.resize((size_t)c->nranks);
+    for (int r = 0; r < c->nranks; ++r) units[r] = std::min(pairs[(size_t)2 * r], pairs[(size_t)2 * r + 1]);
+    return MISORT_OK;
+}
+
+// A relayed raw (or empty) message of `bytes` (a multiple of 4): the size
+// round is relay_sizes with coded = raw.
+int relay_raw(misort_ctx* c, int bit, const void* sbuf, size_t bytes, void* rbuf, size_t rbytes, hipStream_t s) {
+    int rc = c->small.ensure(64);
+    if (rc) return rc;
+    int64_t* d_sz = (int64_t*)c->small.p + 2;
+    const int64_t w2[2] = {(int64_t)(bytes / 4), (int64_t)(bytes / 4)};
+    HIPCHK(hipMemcpyAsync(d_sz, w2, 16, hipMemcpyHostToDevice, s));
+    std::vector<int64_t> pairs, units;
+    if ((rc = relay_sizes(c, d_sz, pairs, units, s))) return rc;
+    return relay_exchange(c, 4, bit, sbuf, bytes, rbuf, rbytes, s, nullptr, &units);
+}
+
 // One compare-split message exchange of k sorted keys each way, delta-coded
 // (codec.hip).  *rkeys receives the partner's k keys (decoded into c->recv, or
 // the raw message in c->enc_recv when the partner sent it uncoded).
@@ -593,26 +641,39 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sb
                           : misort::codec_encode<uint64_t>((const uint64_t*)sbuf, k, (uint32_t*)c->enc_send.p,
                                                            c->codec_scr.p, scr, d_total, s);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "codec_encode: %s", hipGetErrorString(e));
-    uint32_t coded = 0;
-    HIPCHK(hipMemcpyAsync(&coded, d_total, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const bool use = (int64_t)coded < raw_words;
-    const void* msg = use ? c->enc_send.p : sbuf;
-    const size_t mbytes = use ? (size_t)coded * 4 : (size_t)k * w;
-    size_t rb = 0;
+    // every side sends whichever of coded and raw is smaller; the receiver tells
+    // them apart by the size (coded < raw).  The coded word count stays on the
+    // device: the ranks exchange (coded, raw) word counts straight from device
+    // memory, then one host sync serves both the choice and the sizes.
+    int64_t* d_sz = (int64_t*)c->small.p + 2;  // [coded words, raw words]
+    HIPCHK(hipMemsetAsync(d_sz, 0, 16, s));
+    HIPCHK(hipMemcpyAsync(d_sz, d_total, 4, hipMemcpyDeviceToDevice, s));  // low word (little-endian)
+    HIPCHK(hipMemcpyAsync(d_sz + 1, &raw_words, 8, hipMemcpyHostToDevice, s));
+    std::vector<int64_t> all, m;
+    const int me = c->rank;
     if (relayed) {
-        rc = relay_exchange(c, 4, ilog2(q ^ c->rank), msg, mbytes, c->enc_recv.p, c->enc_recv.bytes, s, &rb);
+        if ((rc = relay_sizes(c, d_sz, all, m, s))) return rc;
     } else {
-        // sizes first (8 bytes), then the messages
-        int64_t* d_sz = (int64_t*)c->small.p + 2;
-        const int64_t mine = (int64_t)mbytes;
-        int64_t theirs = 0;
-        HIPCHK(hipMemcpyAsync(d_sz, &mine, 8, hipMemcpyHostToDevice, s));
-        if ((rc = c->tr->sendrecv(d_sz, 8, d_sz + 1, 8, q, s))) return rc;
-        HIPCHK(hipMemcpyAsync(&theirs, d_sz + 1, 8, hipMemcpyDeviceToHost, s));
+        // P = 2 (or no relay): the partner's pair by sendrecv, mine by copy
+        all.assign((size_t)2 * c->nranks, 0);
+        if ((rc = c->tr->sendrecv(d_sz, 16, d_sz + 2, 16, q, s))) return rc;
+        HIPCHK(hipMemcpyAsync(&all[(size_t)2 * me], d_sz, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&all[(size_t)2 * q], d_sz + 2, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (theirs < 0 || (size_t)theirs > c->enc_recv.bytes) return fail(MISORT_E_CAPACITY, "coded message size");
-        rb = (size_t)theirs;
+    }
+    auto units = [&](int r) { return std::min(all[(size_t)2 * r], all[(size_t)2 * r + 1]); };  // 4-byte words sent
+    const bool use = all[(size_t)2 * me] < raw_words;
+    const void* msg = use ? c->enc_send.p : sbuf;
+    const size_t mbytes = (size_t)units(me) * 4;
+    if (mbytes != (use ? (size_t)all[(size_t)2 * me] * 4 : (size_t)k * w))
+        return fail(MISORT_E_INVALID, "coded message size");
+    size_t rb = (size_t)units(q) * 4;
+    if (rb > c->enc_recv.bytes) return fail(MISORT_E_CAPACITY, "coded message size");
+    if (relayed) {
+        size_t rb2 = 0;
+        rc = relay_exchange(c, 4, ilog2(q ^ c->rank), msg, mbytes, c->enc_recv.p, c->enc_recv.bytes, s, &rb2, &m);
+        if (!rc && rb2 != rb) return fail(MISORT_E_INVALID, "relay: partner size mismatch");
+    } else {
         rc = c->tr->sendrecv(msg, mbytes, c->enc_recv.p, rb, q, s);
     }
     if (rc) return rc;
@@ -741,7 +802,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         const bool relayed = c->relay && p > 2;
         if (k == 0) {  // no key crosses: both blocks stay as they are
             // relay units are 4 bytes on every rank of the stage (coded messages are words)
-            if (relayed && (rc = relay_exchange(c, 4, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
+            if (relayed && (rc = relay_raw(c, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
             xg_close(0.0);
             continue;
         }
@@ -768,7 +829,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             // smaller, and the receiver tells them apart by size (coded < raw)
             if ((rc = coded_exchange(c, dtype, q, relayed, sbuf, k, &rkeys, s))) return rc;
         } else {
-            if (relayed) rc = relay_exchange(c, 4, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
+            if (relayed) rc = relay_raw(c, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
             else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
             if (rc) return rc;
             c->xchg_bytes += (int64_t)(sbytes + rbytes);
