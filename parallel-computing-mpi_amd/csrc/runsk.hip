@@ -48,13 +48,14 @@ namespace {
 #endif
 constexpr int FG_LOG2 = MISORT_MK_FG_LOG2;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
-constexpr int CAP = 8192;                       // most keys of a chunk
 #ifndef MISORT_MK_NT
 #define MISORT_MK_NT 512
 #endif
 constexpr int NT = MISORT_MK_NT;         // lanes per chunk workgroup
-constexpr int IT = 9216 / NT;            // keys per lane (NT * IT = 9216 slots for CAP = 8192 plus layout gaps)
-static_assert(NT == 256 || NT == 384 || NT == 512, "chunk workgroup");
+// keys per lane: NT * IT = 9216 slots per 512 lanes' worth (CAP plus layout gaps)
+constexpr int IT = NT >= 512 ? 18 : 9216 / NT;
+static_assert(NT == 256 || NT == 384 || NT == 512 || NT == 1024, "chunk workgroup");
+constexpr int CAP = NT >= 512 ? 16 * NT : 8192;  // most keys of a chunk (8192 at 512 lanes)
 // Every sequence an in-LDS merge reads is followed by G words of MAX
 // (sentinels), so a merge chain needs no end checks: it reads at most IT words
 // past an exhausted sequence.  Each level places its pairs' outputs at lane
@@ -62,7 +63,7 @@ static_assert(NT == 256 || NT == 384 || NT == 512, "chunk workgroup");
 constexpr int G = IT + 1;
 constexpr int PAD = 4;  // words below the tile: a co-rank probe may read index -1
 // 4 tiles of ~34 KiB per CU (LDS); 8 waves per SIMD (<= 64 VGPRs) at NT = 512
-constexpr int WG_PER_CU = 4;
+constexpr int WG_PER_CU = NT == 1024 ? 2 : 4;
 
 template <int LK>
 struct Shape {
@@ -474,15 +475,16 @@ __global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __r
 // steps 2^j <= maxr, a uniform bound on hi - lo <= min(LA, LB) (<= CAP/2 =
 // 2^12), sum to >= hi - lo.  Probe addresses stay inside [A0 - 1, A0 + LA)
 // and [B0, B0 + LB].
+constexpr int CO_STEP0 = CAP / 2;  // first co-rank step: hi - lo <= CAP/2
 __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d, int maxr) {
-    static_assert(CAP / 2 <= 8191, "co-rank steps");
+    static_assert(CAP / 2 <= 2 * CO_STEP0 - 1, "co-rank steps");
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
     const uint32_t* a = s + A0 - 1;
     const uint32_t* b = s + B0 + d;
     int base = lo;
 #pragma unroll
-    for (int step = 4096; step >= 1; step >>= 1) {
+    for (int step = CO_STEP0; step >= 1; step >>= 1) {
         if (step > maxr) continue;  // uniform
         const int i = base + step;
         const int ic = i < hi ? i : hi;
