@@ -83,7 +83,11 @@ struct PlanKnobs {
     // 3 measured best at 2^30: 63.8 Gkeys/s vs 62.6 with 16-way passes (a 4th
     // in-LDS level and 16-way planning cost more than the pass they save)
     int multiway = 3;
+    // the same for u64 (and f64) keys (MISORT_MULTIWAY_U64): 128-bit fences,
+    // 8192-key chunks at 2 workgroups per CU
+    int multiway_u64 = 3;
     PlanKnobs();
+    int multiway_cap(int kb) const { return kb == 4 ? multiway : multiway_u64; }
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
     bool big(int kb) const { return kb == 4 ? tile_u32 == 15 : tile_u64 == 14; }
@@ -1374,13 +1378,16 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
     if (runs && m0 > 0 && k > m0 && !(sizeof(K) == 4 && k <= kn.merge_min_log2_u32)) {
         std::vector<Pass> ps = plan_uncached<K, LT, LTR>(m0 < LT ? LT : m0, false);
         int lw = m0 < LT ? LT : m0;
-        // u32: the levels in as few multi-way passes as the cap allows (a
-        // pass of lk levels is one HBM sweep; runsk.hip needs lw >= 15 and
-        // lw + lk <= 30), the larger ones first; a single level left over
-        // runs as a 2-way pass (which keeps host staging's chunked final pass)
-        if (sizeof(K) == 4 && kn.multiway >= 2 && lw >= 15) {
-            const int cap = kn.multiway < 4 ? kn.multiway : 4;
-            const int L = (k < 30 ? k : 30) - lw;  // levels the multi-way passes can take
+        // the levels in as few multi-way passes as the cap allows (a pass of
+        // lk levels is one HBM sweep; runsk.hip needs lw >= 15 and lw + lk <=
+        // 30 for u32, 13 and 29 for u64), the larger ones first; a single
+        // level left over runs as a 2-way pass (which keeps host staging's
+        // chunked final pass)
+        const int mw = kn.multiway_cap((int)sizeof(K));
+        const int lwk_max = merge_levelk_lwk_max((int)sizeof(K));
+        if (mw >= 2 && lw >= merge_levelk_lw_min((int)sizeof(K))) {
+            const int cap = mw < 4 ? mw : 4;
+            const int L = (k < lwk_max ? k : lwk_max) - lw;  // levels the multi-way passes can take
             if (L >= 2) {
                 const int np = (L + cap - 1) / cap;  // fewest passes
                 for (int i = 0; i < np; ++i) {
@@ -1445,17 +1452,13 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
         if (p.kind == KIND_RUNSK) {
-            if constexpr (sizeof(K) == 4) {
-                const bool prevk = i > 0 && ps[i - 1].kind == KIND_RUNSK;
-                const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
-                const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next);
-                if (e != hipSuccess) return e;
-                fence_phase ^= 1;
-                src = dst;
-                continue;
-            } else {
-                return hipErrorInvalidValue;
-            }
+            const bool prevk = i > 0 && ps[i - 1].kind == KIND_RUNSK;
+            const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
+            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next);
+            if (e != hipSuccess) return e;
+            fence_phase ^= 1;
+            src = dst;
+            continue;
         }
         const bool runs = p.kind == KIND_RUNS;
         const bool contig = p.kind == KIND_TILE_SORT || p.kind == KIND_TILE_MERGE || runs;
@@ -1515,10 +1518,8 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     const int LT = big ? S + 1 : S;
     const Pass p{(Kind)kind, hi, R, flip != 0};
     if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);  // runs of 2^hi -> 2^(hi+1)
-    if (kind == KIND_RUNSK) {  // runs of 2^hi -> 2^(hi+R), R = 1..3 (0: 2)
-        if constexpr (sizeof(K) == 4) return merge_levelk(in, out, n, hi, R > 0 ? R : 2, s, 0, true, 0);
-        return hipErrorInvalidValue;
-    }
+    if (kind == KIND_RUNSK)  // runs of 2^hi -> 2^(hi+R), R = 1..4 (0: 2)
+        return merge_levelk(in, out, n, hi, R > 0 ? R : 2, s, 0, true, 0);
     if (kind < 0 || kind >= KIND_COUNT || kind == KIND_MERGE_SPLIT || kind == KIND_OTHER ||
         kind == KIND_EXCHANGE)
         return hipErrorInvalidValue;

@@ -82,7 +82,7 @@ hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, in
 template <typename K>
 hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0);
 
-// lk merge levels in one HBM pass (runsk.hip, u32, lk = 1..4): src holds
+// lk merge levels in one HBM pass (runsk.hip, u32 and u64, lk = 1..4): src holds
 // ascending runs of 2^lw keys, dst gets ascending runs of 2^(lw+lk) (2^lk-way
 // merge of each group of runs; the last group may be short).  Chunks are cut
 // at fences (every 128th key of a run): `phase` selects which of two
@@ -93,7 +93,13 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
 // aligned.
 hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next);
-int64_t mergek_chunks(int64_t n, int lw, int lk);
+// u64 keys: the same with 128-bit fences (key << 64 | run/position tag);
+// 13 <= lw, lw + lk <= 29.
+hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                        bool gather, int lk_next);
+int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
+int merge_levelk_lw_min(int key_bytes);   // shortest input runs (log2) of a multi-way pass
+int merge_levelk_lwk_max(int key_bytes);  // largest output runs (log2)
 
 // psort.cc:88-101 lower_bound on a sorted device run: *d_out = first i with
 // x <= a[i], or n.

@@ -30,6 +30,7 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_MERGE_FROM_U64", merge_from_u64);
     env("MISORT_MERGE_MIN_LOG2", merge_min_log2_u32);
     env("MISORT_MULTIWAY", multiway);
+    env("MISORT_MULTIWAY_U64", multiway_u64);
     if (tile_u64 != 13) tile_u64 = 14;
     if (rows_tile_u64 != 13 && tile_u64 == 14) rows_tile_u64 = 14;
     if (tile_u64 != 14) rows_tile_u64 = 13;

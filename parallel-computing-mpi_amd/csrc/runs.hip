@@ -50,8 +50,25 @@ struct RunKT<uint64_t> {
 };
 
 
+// fences of the u64 multi-way passes (runsk.hip): key << 64 | run/position tag
+typedef unsigned __int128 u128;
+template <>
+struct RunKT<u128> {
+    static constexpr int IT = 4;
+    static constexpr int NT = 1024;  // 4096-fence tiles, 64 KiB of LDS
+    static constexpr int V = 1;
+    typedef u128 vec;
+};
+
 template <typename K>
 constexpr K KT_MAX = (K)~(K)0;
+
+// lane element e of a vector (a plain value when V = 1)
+template <typename K>
+__device__ __forceinline__ void vset(typename RunKT<K>::vec& x, int e, K v) {
+    if constexpr (RunKT<K>::V == 1) x = v;
+    else x[e] = v;
+}
 
 struct PairGeo {
     int64_t base, na, nb;
@@ -157,7 +174,7 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
         for (int k = 0; k < IT; k += V) {
             vec x;
 #pragma unroll
-            for (int e = 0; e < V; ++e) x[e] = r[k + e];
+            for (int e = 0; e < V; ++e) vset<K>(x, e, r[k + e]);
             *reinterpret_cast<vec*>(s + dk + k) = x;
         }
     } else {
@@ -259,5 +276,6 @@ template hipError_t merge_level<uint32_t>(const uint32_t*, uint32_t*, int64_t, i
                                           int64_t);
 template hipError_t merge_level<uint64_t>(const uint64_t*, uint64_t*, int64_t, int, hipStream_t, int64_t,
                                           int64_t);
+template hipError_t merge_level<u128>(const u128*, u128*, int64_t, int, hipStream_t, int64_t, int64_t);
 
 }  // namespace misort

@@ -1,4 +1,4 @@
-// runsk.hip -- K-way merge passes of the local sort (gfx950, u32 keys):
+// runsk.hip -- K-way merge passes of the local sort (gfx950, u32 and u64 keys):
 // ascending runs of W = 2^lw keys, in groups of K = 2^lk (lk = 1..4), ->
 // ascending runs of K*W.  One HBM read + one HBM write per key for lk merge
 // levels (runs.hip does one level per pass): 2^30 keys past the 2^15-key SORT
@@ -12,11 +12,13 @@
 // per tile (nested searches); instead the chunks are cut at FENCES:
 //
 //   fence   = the key at every FG-th position of a run, packed with its place
-//             as (key << 32 | run-in-group << (32 - lk) | position / FG), so
-//             that u64 order is the total order (key, run, position) -- ties
-//             between equal keys go to the lower run, then the lower position;
+//             as (key << B | run-in-group << (32 - lk) | position / FG), B =
+//             the key's bits, so that the fence's unsigned order (u64 for u32
+//             keys, u128 for u64 keys) is the total order (key, run,
+//             position) -- ties between equal keys go to the lower run, then
+//             the lower position;
 //   chunks  = the fences of a group merged into that total order (k_fence_lds
-//             or lk u64 merge levels), every FM-th one starting a chunk;
+//             or lk fence merge levels), every FM-th one starting a chunk;
 //   bounds  = for a chunk-start fence f of run r0 at position j0*FG, run r0
 //             starts at j0*FG and every other run r at its count of keys
 //             before f, found by a binary search confined to the FG positions
@@ -51,44 +53,95 @@ constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
 #ifndef MISORT_MK_NT
 #define MISORT_MK_NT 512
 #endif
-constexpr int NT = MISORT_MK_NT;         // lanes per chunk workgroup
-// keys per lane: NT * IT = 9216 slots per 512 lanes' worth (CAP plus layout gaps)
-constexpr int IT = NT >= 512 ? 18 : 9216 / NT;
-static_assert(NT == 256 || NT == 384 || NT == 512 || NT == 1024, "chunk workgroup");
-constexpr int CAP = NT >= 512 ? 16 * NT : 8192;  // most keys of a chunk (8192 at 512 lanes)
+typedef unsigned __int128 u128;
+
+// Per key type: the fence type (key bits above 32 bits of run and position),
+// the chunk workgroup (NT lanes x IT keys: CAP keys a chunk at most), the
+// workgroups per CU the LDS tile allows, and the largest fence sub-group
+// merged in LDS (64 KiB).
+template <typename KEY>
+struct KTr;
+template <>
+struct KTr<uint32_t> {
+    typedef uint64_t F;
+    static constexpr int NT = MISORT_MK_NT;
+    static constexpr int IT = NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
+    static constexpr int CAP = NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
+    static constexpr int WG_PER_CU = NT == 1024 ? 2 : 4;    // ~34 KiB tiles; 8 waves per SIMD at NT = 512
+    static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
+    static constexpr int LW_MIN = 15, LWK_MAX = 30;         // runs >= the SORT tile; 32-bit row offsets
+};
+static_assert(KTr<uint32_t>::NT == 256 || KTr<uint32_t>::NT == 384 || KTr<uint32_t>::NT == 512 ||
+                  KTr<uint32_t>::NT == 1024,
+              "chunk workgroup");
+template <>
+struct KTr<uint64_t> {
+    typedef u128 F;
+    static constexpr int NT = 512;
+    static constexpr int IT = 18;
+    static constexpr int CAP = 8192;     // 64 KiB of keys: two tiles per CU, 4 waves per SIMD
+    static constexpr int WG_PER_CU = 2;
+    static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
+    static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
+};
+template <typename KEY>
+constexpr KEY KMAX = (KEY)~(KEY)0;
+
 // Every sequence an in-LDS merge reads is followed by G words of MAX
 // (sentinels), so a merge chain needs no end checks: it reads at most IT words
 // past an exhausted sequence.  Each level places its pairs' outputs at lane
 // boundaries past the previous pair's sentinels (no lane straddles two pairs).
-constexpr int G = IT + 1;
-constexpr int PAD = 4;  // words below the tile: a co-rank probe may read index -1
-// 4 tiles of ~34 KiB per CU (LDS); 8 waves per SIMD (<= 64 VGPRs) at NT = 512
-constexpr int WG_PER_CU = NT == 1024 ? 2 : 4;
+constexpr int PAD = 4;  // keys below the tile: a co-rank probe may read index -1
 
-template <int LK>
+template <typename KEY, int LK>
 struct Shape {
+    typedef KTr<KEY> T;
+    static constexpr int NT = T::NT, IT = T::IT, CAP = T::CAP, G = IT + 1;
     static constexpr int K = 1 << LK;
-    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk: 62 / 60 / 56 / 48
+    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
     static constexpr int RW = LK == 4 ? 64 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
-    static constexpr int LDS_WORDS = PAD + CAP + K * (G + IT) + 16;
+    static constexpr int LDS_KEYS = PAD + CAP + K * (G + IT) + 16;
+    static_assert(FM > 0, "fence stride too coarse for the chunk");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
     static_assert(CAP + (K / 2) * (G + IT) <= NT * IT, "level layout: pairs at lane boundaries");
-    static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS word of a row fits 16 bits");
+    static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS key index of a row fits 16 bits");
 };
 
-typedef uint32_t vec4 __attribute__((ext_vector_type(4)));
-typedef uint32_t vec2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
+template <typename KEY>
+using kvec = KEY __attribute__((ext_vector_type(16 / sizeof(KEY))));  // 16 bytes of keys
+template <typename KEY>
+using kvec2 = KEY __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) { return (uint32_t)(uintptr_t)(const lds_u32*)p; }
-__device__ __forceinline__ uint32_t lds_ld(uint32_t a) { return *(const lds_u32*)(uintptr_t)a; }
+template <typename KEY>
+using lds_t = __attribute__((address_space(3))) KEY;
 
-__device__ __host__ __forceinline__ uint64_t fpack(uint32_t key, int64_t gp, int lw, int lk) {
-    const uint64_t r = (uint64_t)(gp >> lw) & ((1u << lk) - 1);
-    const uint64_t j = (uint64_t)(gp & (((int64_t)1 << lw) - 1)) >> FG_LOG2;
-    return ((uint64_t)key << 32) | (r << (32 - lk)) | j;
+template <typename KEY>
+__device__ __forceinline__ uint32_t lds_addr(const KEY* p) {
+    return (uint32_t)(uintptr_t)(const lds_t<KEY>*)p;
+}
+template <typename KEY>
+__device__ __forceinline__ KEY lds_ld(uint32_t a) {
+    return *(const lds_t<KEY>*)(uintptr_t)a;
+}
+
+// fence <-> (key, tag): tag = run << (32 - lk) | position / FG, the low 32 bits
+template <typename KEY>
+__device__ __host__ __forceinline__ typename KTr<KEY>::F fpack(KEY key, int64_t gp, int lw, int lk) {
+    typedef typename KTr<KEY>::F F;
+    const uint32_t r = (uint32_t)(gp >> lw) & ((1u << lk) - 1);
+    const uint32_t j = (uint32_t)((gp & (((int64_t)1 << lw) - 1)) >> FG_LOG2);
+    return ((F)key << (8 * sizeof(KEY))) | (F)((r << (32 - lk)) | j);
+}
+template <typename F>
+__device__ __forceinline__ auto fkey(F f) {
+    if constexpr (sizeof(F) == 8) return (uint32_t)(f >> 32);
+    else return (uint64_t)(f >> 64);
+}
+template <typename F>
+__device__ __forceinline__ uint32_t ftag(F f) {
+    return (uint32_t)f;
 }
 
 // Group geometry of the pass: groups of K runs of W keys; run r of group g
@@ -116,28 +169,33 @@ struct Geo {
     }
 };
 
+template <typename KEY>
 Geo make_geo(int64_t n, int lw, int lk) {
-    Geo geo{n, lw, lk, CAP / (int)FG - (1 << lk), 0, 0};
+    Geo geo{n, lw, lk, KTr<KEY>::CAP / (int)FG - (1 << lk), 0, 0};
     geo.nfull = n >> (lw + lk);
     geo.kf = ((((int64_t)1 << (lw + lk)) >> FG_LOG2) + geo.fm - 1) / geo.fm;
     return geo;
 }
 
 // F[i] = fence of position i*FG (the first multi-way pass after the SORT tile).
-__global__ void k_fence_gather(const uint32_t* __restrict__ src, int64_t n, int lw, int lk, uint64_t* __restrict__ F) {
+template <typename KEY>
+__global__ void k_fence_gather(const KEY* __restrict__ src, int64_t n, int lw, int lk,
+                               typename KTr<KEY>::F* __restrict__ F) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
     if (i >= nf) return;
     const int64_t gp = i << FG_LOG2;
-    F[i] = fpack(src[gp], gp, lw, lk);
+    F[i] = fpack<KEY>(src[gp], gp, lw, lk);
 }
 
-// Runs of 2^wf fences merged 2^a at a time (<= 8192 fences) into total order
-// in LDS: block b takes fences [b << (wf + a), ...); each fence's rank = its
-// index in its run's list + its lower bound in the sub-group's other runs.
-__global__ __launch_bounds__(1024) void k_fence_lds(const uint64_t* __restrict__ F, uint64_t* __restrict__ M,
-                                                    int64_t nf, int wf_log2, int a) {
-    extern __shared__ uint64_t sf[];
+// Runs of 2^wf fences merged 2^a at a time (<= 64 KiB of fences) into total
+// order in LDS: block b takes fences [b << (wf + a), ...); each fence's rank =
+// its index in its run's list + its lower bound in the sub-group's other runs.
+template <typename FT>
+__global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT* __restrict__ M, int64_t nf,
+                                                    int wf_log2, int a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sraw[];
+    FT* sf = reinterpret_cast<FT*>(sraw);
     const int64_t f0 = (int64_t)blockIdx.x << (wf_log2 + a);
     const int nfg = (int)((nf - f0) < ((int64_t)1 << (wf_log2 + a)) ? nf - f0 : ((int64_t)1 << (wf_log2 + a)));
     const int wf = 1 << wf_log2;
@@ -145,7 +203,7 @@ __global__ __launch_bounds__(1024) void k_fence_lds(const uint64_t* __restrict__
     for (int e = threadIdx.x; e < nfg; e += blockDim.x) sf[e] = F[f0 + e];
     __syncthreads();
     for (int e = threadIdx.x; e < nfg; e += blockDim.x) {
-        const uint64_t v = sf[e];
+        const FT v = sf[e];
         const int r = e / wf;
         int rank = e - r * wf;
         for (int q = 0; q < K; ++q) {
@@ -198,7 +256,8 @@ __device__ __forceinline__ int block_scan(int v, int* sw) {
 // fences before a chunk-start fence = P(c) - P(group's first chunk), with the
 // block totals scanned in (k_scan_totals) -- this replaces a binary search of
 // each run's fence list.
-__global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const uint64_t* __restrict__ M, Geo geo, int64_t nchunks,
+template <typename FT>
+__global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
                                                           int* __restrict__ P, int* __restrict__ bsum) {
     __shared__ int sw[SCAN_NT / 64];
     const int64_t c = (int64_t)blockIdx.x * SCAN_NT + threadIdx.x;
@@ -207,11 +266,11 @@ __global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const uint64_t* __rest
     if (c < nchunks) {
         int64_t g, t;
         chunk_place(geo, c, g, t);
-        const uint64_t* m = M + (geo.base(g) >> FG_LOG2);
+        const FT* m = M + (geo.base(g) >> FG_LOG2);
         const int64_t e0 = t * geo.fm, nf = geo.nfences(g);
         const int64_t e1 = e0 + geo.fm < nf ? e0 + geo.fm : nf;
         for (int64_t e = e0; e < e1; ++e) {
-            const int r = (int)((m[e] >> (32 - geo.lk)) & (K - 1));
+            const int r = (int)((ftag(m[e]) >> (32 - geo.lk)) & (K - 1));
 #pragma unroll
             for (int q = 0; q < 16; ++q) cnt[q] += q == r;
         }
@@ -242,13 +301,26 @@ __global__ __launch_bounds__(SCAN_NT) void k_scan_totals(int* __restrict__ bsum,
     }
 }
 
+// Interpolated guess of where v falls between positions a and b whose keys
+// are ka < kb.
+template <typename KEY>
+__device__ __forceinline__ int64_t interp(KEY v, KEY ka, KEY kb, int64_t a, int64_t b) {
+    if constexpr (sizeof(KEY) == 4) {
+        return a + (int64_t)(((uint64_t)(v - ka) * (uint64_t)(b - a)) / (uint64_t)(kb - ka));
+    } else {
+        return a + (int64_t)((double)(v - ka) / (double)(kb - ka) * (double)(b - a));
+    }
+}
+
 // One thread per (bounds slot, run): the start of chunk t of group g in run r
 // (a position within the run), or the run's length for the group's end slot.
 // Run r's fences before the chunk-start fence f come from the scanned counts;
 // the keys before f lie among the FG positions after the last of them.
-__global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __restrict__ F,
-                         const uint64_t* __restrict__ M, const int* __restrict__ P, const int* __restrict__ bsum,
-                         Geo geo, int64_t nslots, int64_t* __restrict__ bounds) {
+template <typename KEY>
+__global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                         const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                         const int* __restrict__ bsum, Geo geo, int64_t nslots, int64_t* __restrict__ bounds) {
+    typedef typename KTr<KEY>::F FT;
     const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= (nslots << geo.lk)) return;
     const int64_t s = id >> geo.lk;
@@ -266,11 +338,11 @@ __global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __res
         bounds[id] = len;
         return;
     }
-    const uint64_t f = M[(base >> FG_LOG2) + t * geo.fm];
-    const uint32_t v = (uint32_t)(f >> 32);
-    const int r0 = (int)((f >> (32 - geo.lk)) & (geo.K() - 1));
+    const FT f = M[(base >> FG_LOG2) + t * geo.fm];
+    const KEY v = (KEY)fkey(f);
+    const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (geo.K() - 1));
     if (r == r0) {
-        bounds[id] = (int64_t)(f & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
+        bounds[id] = (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
         return;
     }
     if (len == 0) {
@@ -297,19 +369,19 @@ __global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __res
     // on spread keys the probes stay within a line or two of the answer
     // (a plain binary search touches ~5 lines of the 1 KiB window; the kernel
     // is bound by those probe lines).
-    const uint32_t* kr = src + base + r * W;
-    const uint64_t* fr = F + ((base + r * W) >> FG_LOG2);
+    const KEY* kr = src + base + r * W;
+    const FT* fr = F + ((base + r * W) >> FG_LOG2);
     const int64_t a = ((lo - 1) << FG_LOG2) + 1, b = (lo << FG_LOG2) < len ? (lo << FG_LOG2) : len;
     const bool le = r < r0;
     auto before = [&](int64_t q) {
-        const uint32_t k = kr[q];
+        const KEY k = kr[q];
         return le ? k <= v : k < v;
     };
-    const uint32_t ka = (uint32_t)(fr[lo - 1] >> 32);
+    const KEY ka = (KEY)fkey(fr[lo - 1]);
     int64_t p = a + ((b - a) >> 1);
     if ((lo << FG_LOG2) < len) {
-        const uint32_t kb = (uint32_t)(fr[lo] >> 32);
-        if (kb > ka) p = a + (int64_t)(((uint64_t)(v - ka) * (uint64_t)(b - a)) / (uint64_t)(kb - ka));
+        const KEY kb = (KEY)fkey(fr[lo]);
+        if (kb > ka) p = interp<KEY>(v, ka, kb, a, b);
     }
     p = p < a ? a : (p > b ? b : p);
     int64_t lo_b, hi_b;  // the answer lies in [lo_b, hi_b]
@@ -353,19 +425,19 @@ __global__ void k_bounds(const uint32_t* __restrict__ src, const uint64_t* __res
 // loaded in NROWS rows of RW consecutive keys, each row inside one segment
 // (segment r takes ceil(l_r / RW) rows; the K take <= CAP/RW + K = NROWS):
 // row j = byte offset of its first key from the group base, and how many of
-// its RW keys are real plus the LDS word the first goes to (segment r's keys
-// start at LDS word o_r + r*G, leaving G words for sentinels after each).
+// its RW keys are real plus the LDS slot the first goes to (segment r's keys
+// start at LDS slot o_r + r*G, leaving G slots for sentinels after each).
 // The tables are stored by part: entry p*IT + j is row j*NR + p, so a wave
 // reads its IT entries as a few wide scalar loads.
 // Validated so that no chunk can address memory outside its group's runs:
 // a bad chunk gets no rows and is left unwritten (the sort then fails its
 // checks).
-template <int LK>
+template <typename KEY, int LK>
 struct alignas(128) Desc {  // whole 128-byte lines: a chunk's entries never share a line with another's
     int64_t gbase, out0;
-    int o[Shape<LK>::K + 1];           // chunk position of segment r; o[K] = chunk length
-    uint32_t off[Shape<LK>::NROWS];  // byte offset of the row's first key from the group base
-    uint32_t la[Shape<LK>::NROWS];   // real keys of the row (0..RW) | LDS word of its first key << 16
+    int o[Shape<KEY, LK>::K + 1];           // chunk position of segment r; o[K] = chunk length
+    uint32_t off[Shape<KEY, LK>::NROWS];  // byte offset of the row's first key from the group base
+    uint32_t la[Shape<KEY, LK>::NROWS];   // real keys of the row (0..RW) | LDS slot of its first key << 16
 };
 
 // One wave per DESC_CPW consecutive chunks (DESC_CPB waves per workgroup):
@@ -374,17 +446,17 @@ struct alignas(128) Desc {  // whole 128-byte lines: a chunk's entries never sha
 // the lanes write the table entries.
 constexpr int DESC_CPB = 4, DESC_CPW = 4;
 
-template <int LK>
+template <typename KEY, int LK>
 __device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, int lane, int64_t st, int64_t en,
-                                         Desc<LK>* __restrict__ desc) {
-    typedef Shape<LK> S;
+                                         Desc<KEY, LK>* __restrict__ desc) {
+    typedef Shape<KEY, LK> S;
     constexpr int K = S::K;
     const int64_t ln = en - st;
     bool ok = true;
-    if (lane < K) ok = st >= 0 && ln >= 0 && en <= geo.run_len(g, lane) && ln <= CAP;
+    if (lane < K) ok = st >= 0 && ln >= 0 && en <= geo.run_len(g, lane) && ln <= S::CAP;
     // bounds outside the runs would be a logic error: never let them address memory
     ok = __all(ok);
-    // the K lanes' values as scalars (starts < W <= 2^27 and lengths <= CAP fit 32 bits)
+    // the K lanes' values as scalars (starts < W <= 2^28 and lengths <= CAP fit 32 bits)
     int sln[K], sst[K];
     int tot = 0;
 #pragma unroll
@@ -393,9 +465,9 @@ __device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, i
         sst[r] = __builtin_amdgcn_readlane((int)st, r);
         tot += sln[r];
     }
-    ok = ok && tot <= CAP;
+    ok = ok && tot <= S::CAP;
     int srow[K + 1], so[K + 1];
-    uint32_t sb[K];  // byte offset of segment r's first key from the group base (< KW*4 <= 2^32)
+    uint32_t sb[K];  // byte offset of segment r's first key from the group base (< KW*sizeof(KEY) <= 2^32)
     int R = 0, o = 0;
     int64_t out = geo.base(g);
 #pragma unroll
@@ -403,14 +475,14 @@ __device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, i
         if (!ok) sln[r] = sst[r] = 0;
         srow[r] = R;
         so[r] = o;
-        sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)sst[r]) * 4u;
+        sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)sst[r]) * (uint32_t)sizeof(KEY);
         R += (sln[r] + S::RW - 1) / S::RW;
         o += sln[r];
         out += sst[r];
     }
     srow[K] = R;
     so[K] = o;
-    Desc<LK>& d = desc[c];
+    Desc<KEY, LK>& d = desc[c];
     if (lane == 0) {
         d.gbase = geo.base(g);
         d.out0 = out;
@@ -419,7 +491,7 @@ __device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, i
     for (int r = 0; r <= K; ++r)
         if (lane == r) d.o[r] = so[r];
     for (int j = lane; j < S::NROWS; j += 64) {
-        const int row = (j % IT) * S::NR + j / IT;  // table entry j (stored by part)
+        const int row = (j % S::IT) * S::NR + j / S::IT;  // table entry j (stored by part)
         // the row's segment: the last one starting at or before it
         int rr = 0;
 #pragma unroll
@@ -431,21 +503,21 @@ __device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, i
             if (rr == r) {
                 rs = srow[r];
                 rl = sln[r];
-                rb = so[r] + r * G;
+                rb = so[r] + r * S::G;
                 ro = sb[r];
             }
         }
         const int k = row - rs, rem = rl - k * S::RW;
         const bool in = row < srow[K];  // rows past the chunk: no keys
-        d.off[j] = in ? ro + (uint32_t)(k * S::RW * 4) : 0u;
+        d.off[j] = in ? ro + (uint32_t)(k * S::RW * (int)sizeof(KEY)) : 0u;
         d.la[j] = in ? (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(rb + k * S::RW) << 16) : 0u;
     }
 }
 
-template <int LK>
+template <typename KEY, int LK>
 __global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo,
-                                                             int64_t nchunks, Desc<LK>* __restrict__ desc) {
-    constexpr int K = Shape<LK>::K;
+                                                             int64_t nchunks, Desc<KEY, LK>* __restrict__ desc) {
+    constexpr int K = Shape<KEY, LK>::K;
     const int64_t c0 = ((int64_t)blockIdx.x * DESC_CPB + (threadIdx.x >> 6)) * DESC_CPW;
     const int lane = threadIdx.x & 63;
     int64_t g[DESC_CPW], st[DESC_CPW], en[DESC_CPW];
@@ -464,7 +536,7 @@ __global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __r
     }
 #pragma unroll
     for (int i = 0; i < DESC_CPW; ++i)
-        if (c0 + i < nchunks) desc_one<LK>(geo, c0 + i, g[i], lane, st[i], en[i], desc);
+        if (c0 + i < nchunks) desc_one<KEY, LK>(geo, c0 + i, g[i], lane, st[i], en[i], desc);
 }
 
 // Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
@@ -475,13 +547,13 @@ __global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __r
 // steps 2^j <= maxr, a uniform bound on hi - lo <= min(LA, LB) (<= CAP/2 =
 // 2^12), sum to >= hi - lo.  Probe addresses stay inside [A0 - 1, A0 + LA)
 // and [B0, B0 + LB].
-constexpr int CO_STEP0 = CAP / 2;  // first co-rank step: hi - lo <= CAP/2
-__device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0, int LB, int d, int maxr) {
-    static_assert(CAP / 2 <= 2 * CO_STEP0 - 1, "co-rank steps");
+template <typename KEY>
+__device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
+    constexpr int CO_STEP0 = KTr<KEY>::CAP / 2;  // first co-rank step: hi - lo <= CAP/2
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
-    const uint32_t* a = s + A0 - 1;
-    const uint32_t* b = s + B0 + d;
+    const KEY* a = s + A0 - 1;
+    const KEY* b = s + B0 + d;
     int base = lo;
 #pragma unroll
     for (int step = CO_STEP0; step >= 1; step >>= 1) {
@@ -499,57 +571,69 @@ __device__ __forceinline__ int co_rank(const uint32_t* s, int A0, int LA, int B0
 // last, and g, the other side's head: each step outputs min(h, g), keeps
 // max(h, g) as the other head and reads the next key of the side it took
 // (swapping the two read pointers when that side changes) -- six VALU ops and
-// one LDS read per output.  Ties may go either way: equal keys are identical.
-// Past the end of both sequences a chain outputs MAX (their sentinels).
-__device__ __forceinline__ void merge_chain(const uint32_t* s, int A0, int LA, int B0, int LB, int d, int maxr,
-                                            uint32_t (&r)[IT]) {
+// one LDS read per output (u32).  Ties may go either way: equal keys are
+// identical.  Past the end of both sequences a chain outputs MAX (their
+// sentinels).
+template <typename KEY, int IT>
+__device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                            KEY (&r)[IT]) {
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
-    const int ia = co_rank(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
     // byte addresses of the two heads (LDS pointers are 32-bit)
-    uint32_t px = lds_addr(s + A0 + ia), py = lds_addr(s + B0 + dc - ia);
-    uint32_t h = lds_ld(px), g = lds_ld(py);
+    uint32_t px = lds_addr<KEY>(s + A0 + ia), py = lds_addr<KEY>(s + B0 + dc - ia);
+    KEY h = lds_ld<KEY>(px), g = lds_ld<KEY>(py);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const bool keep = h <= g;
-        r[k] = min(h, g);
-        const uint32_t o = max(h, g);
+        KEY o;
+        if constexpr (sizeof(KEY) == 4) {
+            r[k] = min(h, g);
+            o = max(h, g);
+        } else {  // no 64-bit min/max: selects on the one compare
+            r[k] = keep ? h : g;
+            o = keep ? g : h;
+        }
         const uint32_t nx = keep ? px : py;
         py = keep ? py : px;
-        px = nx + 4;
-        h = lds_ld(px);
+        px = nx + (uint32_t)sizeof(KEY);
+        h = lds_ld<KEY>(px);
         g = o;
     }
 }
 
 // The wave's row part (uniform) and the lane's place in its row.
-template <int LK>
-__device__ __forceinline__ int row_part(int tid) { return __builtin_amdgcn_readfirstlane(tid) / Shape<LK>::RW; }
+template <typename KEY, int LK>
+__device__ __forceinline__ int row_part(int tid) {
+    return __builtin_amdgcn_readfirstlane(tid) / Shape<KEY, LK>::RW;
+}
 
 // k_mergek: one workgroup per chunk.  MODE (probes only, MISORT_MK_PROBE):
 // 0 = the pass; 1 = no merge (the access pattern's floor); 2 = level 1 only.
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
-template <int LK, bool FENCES, int MODE = 0>
-__global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint32_t* __restrict__ src,
-                                                                      uint32_t* __restrict__ dst,
-                                                                      const Desc<LK>* __restrict__ desc,
-                                                                      uint64_t* __restrict__ fout, int lwn, int lkn) {
-    typedef Shape<LK> S;
-    constexpr int K = S::K;
-    constexpr int LAST = S::LDS_WORDS - PAD - 1;
-    __shared__ __attribute__((aligned(16))) uint32_t tile[S::LDS_WORDS];
-    uint32_t* s = tile + PAD;
+template <typename KEY, int LK, bool FENCES, int MODE = 0>
+__global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 256) void k_mergek(
+    const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
+    typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
+    typedef Shape<KEY, LK> S;
+    constexpr int K = S::K, NT = S::NT, IT = S::IT, G = S::G;
+    constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
+    constexpr int LAST = S::LDS_KEYS - PAD - 1;
+    constexpr KEY MAXK = KMAX<KEY>;
+    __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
+    KEY* s = tile + PAD;
     const int tid = threadIdx.x;
-    const Desc<LK>* d = desc + blockIdx.x;
+    const Desc<KEY, LK>* d = desc + blockIdx.x;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
         // table entries first (scalar registers), then all its loads
         const char* gsrc = (const char*)(src + d->gbase);
-        const int part = row_part<LK>(tid), lt = tid & (S::RW - 1);
+        const int part = row_part<KEY, LK>(tid), lt = tid & (S::RW - 1);
         const uint32_t* offp = d->off + part * IT;
         const uint32_t* lap = d->la + part * IT;
-        uint32_t off[IT], la[IT], x[IT];
+        uint32_t off[IT], la[IT];
+        KEY x[IT];
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             off[j] = offp[j];
@@ -558,18 +642,18 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
 #pragma unroll
         for (int j = 0; j < IT; ++j)
             if (lt < (int)(la[j] & 0xFFFF))
-                x[j] = __builtin_nontemporal_load((const uint32_t*)(gsrc + off[j]) + (uint32_t)lt);
+                x[j] = __builtin_nontemporal_load((const KEY*)(gsrc + off[j]) + (uint32_t)lt);
 #pragma unroll
         for (int j = 0; j < IT; ++j)
             if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         if (tid < K * G) {  // the sentinels after every segment
             const int r = tid / G;
-            s[d->o[r + 1] + r * G + (tid - r * G)] = 0xFFFFFFFFu;
+            s[d->o[r + 1] + r * G + (tid - r * G)] = MAXK;
         }
     }
     __syncthreads();
     const int len = d->o[K];
-    uint32_t r[IT];
+    KEY r[IT];
     const int pos = tid * IT;
     const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
     // the current level's input sequences (uniform): start and length
@@ -611,7 +695,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            merge_chain(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         __syncthreads();
         if (lv < LK) {
@@ -619,14 +703,14 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
             // the sentinels), the value the sentinel stores write there too
             if (pos < Q + LP) {
 #pragma unroll
-                for (int j = 0; j < IT; j += 2) *reinterpret_cast<vec2*>(s + pos + j) = vec2{r[j], r[j + 1]};
+                for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
             }
             if (tid < P * G) {
                 const int p = tid / G;
                 int e = 0;
 #pragma unroll
                 for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
-                s[e + (tid - p * G)] = 0xFFFFFFFFu;
+                s[e + (tid - p * G)] = MAXK;
             }
             __syncthreads();
 #pragma unroll
@@ -636,37 +720,37 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_mergek(const uint3
             }
         }
     }
-    // the chunk goes to LDS shifted by out0 mod 4, so every global 16-byte
+    // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
     // land past the chunk)
     const int64_t out0 = d->out0;
-    const int sh = (int)(out0 & 3);
+    const int sh = (int)(out0 & (VK - 1));
     if (pos < len) {
-        uint32_t* q = s + sh + pos;
+        KEY* q = s + sh + pos;
 #pragma unroll
         for (int j = 0; j < IT; ++j) q[j] = r[j];
     }
     __syncthreads();
-    const int nv = (sh + len + 3) >> 2;
-    uint32_t* __restrict__ o = dst + (out0 - sh);
+    const int nv = (sh + len + VK - 1) / VK;
+    KEY* __restrict__ o = dst + (out0 - sh);
     for (int v = tid; v < nv; v += NT) {
-        const int e = 4 * v;
-        if (e >= sh && e + 4 <= sh + len) {
-            __builtin_nontemporal_store(*reinterpret_cast<const vec4*>(s + e), reinterpret_cast<vec4*>(o + e));
+        const int e = VK * v;
+        if (e >= sh && e + VK <= sh + len) {
+            __builtin_nontemporal_store(*reinterpret_cast<const kvec<KEY>*>(s + e), reinterpret_cast<kvec<KEY>*>(o + e));
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < VK; ++j)
                 if (e + j >= sh && e + j < sh + len) o[e + j] = s[e + j];
         }
     }
     if constexpr (FENCES) {
         // the chunk's fences are consecutive entries of fout: one coalesced
-        // 8-byte store per fence from consecutive lanes
+        // store per fence from consecutive lanes
         const int64_t first = (out0 + FG - 1) & ~(FG - 1);
         const int nf = first < out0 + len ? (int)((out0 + len - first + FG - 1) >> FG_LOG2) : 0;
         if (tid < nf) {
             const int64_t gp = first + ((int64_t)tid << FG_LOG2);
-            fout[gp >> FG_LOG2] = fpack(s[(int)(gp - (out0 - sh))], gp, lwn, lkn);
+            fout[gp >> FG_LOG2] = fpack<KEY>(s[(int)(gp - (out0 - sh))], gp, lwn, lkn);
         }
     }
 }
@@ -702,87 +786,108 @@ int64_t chunks_of(const Geo& geo) {
     return geo.nfull * geo.kf + (tail ? geo.nchunks(geo.nfull) : 0);
 }
 
-template <int LK>
-hipError_t merge_pass(const uint32_t* src, uint32_t* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
+template <typename KEY, int LK>
+hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
                       int lk_next) {
-    typedef Shape<LK> S;
-    const Geo geo = make_geo(n, lw, LK);
+    typedef Shape<KEY, LK> S;
+    typedef typename KTr<KEY>::F FT;
+    const Geo geo = make_geo<KEY>(n, lw, LK);
     const bool tail = (geo.nfull << (lw + LK)) < n;
     const int64_t nchunks = chunks_of(geo);
     const int64_t nslots = geo.nfull * (geo.kf + 1) + (tail ? geo.nchunks(geo.nfull) + 1 : 0);
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
     if (nchunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     // fence buffers 0 and 1 (kept across passes); per pass: merged fences,
-    // u64 merge temp, bounds, fence counts and their block totals, descriptors
+    // fence merge temp, bounds, fence counts and their block totals, descriptors
     const int64_t nbk = (nchunks + SCAN_NT - 1) / SCAN_NT;
-    const size_t fb = ((size_t)nf * 8 + 255) & ~(size_t)255;
+    const size_t fb = ((size_t)nf * sizeof(FT) + 255) & ~(size_t)255;
     const size_t bb = ((size_t)nslots * S::K * 8 + 255) & ~(size_t)255;
     const size_t cb = ((size_t)nbk * SCAN_NT * S::K * 4 + 255) & ~(size_t)255;
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
     char* fbase = (char*)scratch(0, 2 * fb, s);
-    char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<LK>) + 256, s);
+    char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
     if (!base || !fbase) return hipErrorOutOfMemory;
-    uint64_t* F = (uint64_t*)(fbase + (phase & 1) * fb);
-    uint64_t* Fn = (uint64_t*)(fbase + ((phase & 1) ^ 1) * fb);
-    uint64_t* M = (uint64_t*)base;
-    uint64_t* T = (uint64_t*)(base + fb);
+    FT* F = (FT*)(fbase + (phase & 1) * fb);
+    FT* Fn = (FT*)(fbase + ((phase & 1) ^ 1) * fb);
+    FT* M = (FT*)base;
+    FT* T = (FT*)(base + fb);
     int64_t* bounds = (int64_t*)(base + 2 * fb);
     int* cnt = (int*)(base + 2 * fb + bb);
     int* bsum = (int*)(base + 2 * fb + bb + cb);
-    Desc<LK>* desc = (Desc<LK>*)(base + 2 * fb + bb + cb + sb);
-    if (gather) k_fence_gather<<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
+    Desc<KEY, LK>* desc = (Desc<KEY, LK>*)(base + 2 * fb + bb + cb + sb);
+    if (gather) k_fence_gather<KEY><<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
     const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
     {
         // the group's fences into total order, landing in M: the first a levels
-        // in LDS (sub-groups of 2^a runs, <= 8192 fences = 64 KiB), the other
-        // LK - a as u64 merge levels (runs of >= 2^13 fences), ping-ponging
+        // in LDS (sub-groups of 2^a runs, <= 64 KiB of fences), the other
+        // LK - a as fence merge levels (runs of >= 2^FL fences), ping-ponging
         // through T
-        const int a = wf_log2 >= 13 ? 0 : (13 - wf_log2 < LK ? 13 - wf_log2 : LK);
-        const uint64_t* x = F;
+        constexpr int FL = KTr<KEY>::FL_LDS;
+        const int a = wf_log2 >= FL ? 0 : (FL - wf_log2 < LK ? FL - wf_log2 : LK);
+        const FT* x = F;
         int left = LK - a;
         if (a > 0) {
-            uint64_t* y = (left & 1) ? T : M;
-            const size_t lds = ((size_t)1 << (wf_log2 + a)) * 8;
+            FT* y = (left & 1) ? T : M;
+            const size_t lds = ((size_t)1 << (wf_log2 + a)) * sizeof(FT);
             const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
-            k_fence_lds<<<(unsigned)nb0, 1024, lds, s>>>(F, y, nf, wf_log2, a);
+            k_fence_lds<FT><<<(unsigned)nb0, 1024, lds, s>>>(F, y, nf, wf_log2, a);
             x = y;
         }
         for (int l = a; l < LK; ++l, --left) {
-            uint64_t* y = ((left - 1) & 1) ? T : M;
-            const hipError_t e = merge_level<uint64_t>(x, y, nf, wf_log2 + l, s);
+            FT* y = ((left - 1) & 1) ? T : M;
+            const hipError_t e = merge_level<FT>(x, y, nf, wf_log2 + l, s);
             if (e != hipSuccess) return e;
             x = y;
         }
     }
     const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
-    k_fence_counts<<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    k_fence_counts<FT><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
-    k_bounds<<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots, bounds);
-    k_chunk_desc<LK><<<(unsigned)((nchunks + DESC_CPB * DESC_CPW - 1) / (DESC_CPB * DESC_CPW)), 64 * DESC_CPB, 0, s>>>(
-        bounds, geo, nchunks, desc);
+    k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots,
+                                                                          bounds);
+    k_chunk_desc<KEY, LK>
+        <<<(unsigned)((nchunks + DESC_CPB * DESC_CPW - 1) / (DESC_CPB * DESC_CPW)), 64 * DESC_CPB, 0, s>>>(
+            bounds, geo, nchunks, desc);
     const unsigned grid = (unsigned)nchunks;
-    if (lk_next > 0) k_mergek<LK, true><<<grid, NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
-    else k_mergek<LK, false><<<grid, NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
+    if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
+    else k_mergek<KEY, LK, false><<<grid, S::NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
     if (probe) {
         // same chunks, outputs to a scratch buffer (the sort is untouched)
-        static uint32_t* junk = nullptr;
+        static KEY* junk = nullptr;
         static size_t junk_n = 0;
         if (junk_n < (size_t)n) {
             if (junk) (void)hipFree(junk);
             junk = nullptr;
-            if (hipMalloc(&junk, (size_t)n * 4) != hipSuccess) return hipErrorOutOfMemory;
+            if (hipMalloc(&junk, (size_t)n * sizeof(KEY)) != hipSuccess) return hipErrorOutOfMemory;
             junk_n = (size_t)n;
         }
-        k_mergek<LK, false, 1><<<grid, NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
-        k_mergek<LK, false, 2><<<grid, NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+        k_mergek<KEY, LK, false, 1><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+        k_mergek<KEY, LK, false, 2><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
     }
     return hipGetLastError();
 }
 
+template <typename KEY>
+hipError_t merge_levelk_t(const KEY* src, KEY* dst, int64_t n, int lw, int lk, hipStream_t s, int phase, bool gather,
+                          int lk_next) {
+    if (n <= 0) return hipSuccess;
+    // load rows address a group with 32-bit byte offsets (KW * sizeof(KEY) <=
+    // 2^32); runs at least a SORT tile long
+    if (lk < 1 || lk > 4 || lw < KTr<KEY>::LW_MIN || lw + lk > KTr<KEY>::LWK_MAX || src == dst || lk_next < 0 ||
+        lk_next > 4)
+        return hipErrorInvalidValue;
+    if (lk == 1) return merge_pass<KEY, 1>(src, dst, n, lw, s, phase, gather, lk_next);
+    if (lk == 2) return merge_pass<KEY, 2>(src, dst, n, lw, s, phase, gather, lk_next);
+    if (lk == 3) return merge_pass<KEY, 3>(src, dst, n, lw, s, phase, gather, lk_next);
+    return merge_pass<KEY, 4>(src, dst, n, lw, s, phase, gather, lk_next);
+}
+
 }  // namespace
 
-int64_t mergek_chunks(int64_t n, int lw, int lk) { return chunks_of(make_geo(n, lw, lk)); }
+int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes) {
+    return key_bytes == 8 ? chunks_of(make_geo<uint64_t>(n, lw, lk)) : chunks_of(make_geo<uint32_t>(n, lw, lk));
+}
 
 // phase: which of the two fence buffers holds this pass's input fences
 // (gather: build them from src first); lk_next > 0: write the next multi-way
@@ -790,15 +895,13 @@ int64_t mergek_chunks(int64_t n, int lw, int lk) { return chunks_of(make_geo(n, 
 // buffer.
 hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next) {
-    if (n <= 0) return hipSuccess;
-    // load rows address a group with 32-bit byte offsets (KW*4 <= 2^32); runs
-    // at least a 2^15 SORT tile long
-    if (lk < 1 || lk > 4 || lw < 15 || lw + lk > 30 || src == dst || lk_next < 0 || lk_next > 4)
-        return hipErrorInvalidValue;
-    if (lk == 1) return merge_pass<1>(src, dst, n, lw, s, phase, gather, lk_next);
-    if (lk == 2) return merge_pass<2>(src, dst, n, lw, s, phase, gather, lk_next);
-    if (lk == 3) return merge_pass<3>(src, dst, n, lw, s, phase, gather, lk_next);
-    return merge_pass<4>(src, dst, n, lw, s, phase, gather, lk_next);
+    return merge_levelk_t<uint32_t>(src, dst, n, lw, lk, s, phase, gather, lk_next);
 }
+hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                        bool gather, int lk_next) {
+    return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next);
+}
+int merge_levelk_lw_min(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LW_MIN : KTr<uint32_t>::LW_MIN; }
+int merge_levelk_lwk_max(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LWK_MAX : KTr<uint32_t>::LWK_MAX; }
 
 }  // namespace misort

@@ -97,32 +97,45 @@ def test_merge_level_duplicates_and_single_run(ctx, dt):
 
 
 @pytest.mark.parametrize("lk", [1, 2, 3, 4])
-@pytest.mark.parametrize("hi", [15, 16, 17])
+@pytest.mark.parametrize("dt,hi", [(np.uint32, 15), (np.uint32, 16), (np.uint32, 17), (np.uint64, 13),
+                                   (np.uint64, 14), (np.uint64, 16)])
 @pytest.mark.parametrize("n", [(1 << 20) + 3, (1 << 19), (1 << 19) - 4097, 3 * (1 << 17) + 5, 5000, 12345, 2049])
-def test_mergek_level_matches_numpy(ctx, lk, hi, n):
+def test_mergek_level_matches_numpy(ctx, lk, dt, hi, n):
     """One 2^lk-way pass (runsk.hip): groups of 2^lk runs merged, ragged last
-    group (1 to 2^lk runs, the last one short), fences gathered from the runs."""
-    x = runs_input(n, hi, np.uint32, n + hi + lk)
+    group (1 to 2^lk runs, the last one short), fences gathered from the runs;
+    u32 keys with 64-bit fences, u64 keys with 128-bit fences."""
+    x = runs_input(n, hi, dt, n + hi + lk)
     np.testing.assert_array_equal(run_level(ctx, x, hi, "run_mergek", lk), expectk(x, hi, lk))
 
 
 @pytest.mark.parametrize("lk", [1, 2, 3, 4])
-@pytest.mark.parametrize("hi", [15, 16, 21])
-def test_mergek_level_ties_and_edges(ctx, lk, hi):
+@pytest.mark.parametrize("dt,hi", [(np.uint32, 15), (np.uint32, 16), (np.uint32, 21), (np.uint64, 13),
+                                   (np.uint64, 16), (np.uint64, 19)])
+def test_mergek_level_ties_and_edges(ctx, lk, dt, hi):
     """Duplicate-heavy, all-equal (every fence the same key: chunks cut by
-    (run, position)), presorted and interleaved runs; hi = 21 merges the
-    fences with lk u64 merge levels instead of in LDS."""
+    (run, position)), presorted and interleaved runs; hi = 21 (u32) / 19 (u64)
+    merges the fences with lk fence merge levels instead of in LDS.  u64
+    cases put distinct high words above equal low words, so a fence that
+    compared only 32 bits of the key would cut the chunks wrongly."""
     K = 1 << lk
     n = (K << hi) + ((K - 1) << hi) + 1000  # one full group + a (K-1)-run tail
-    cases = [runs_input(n, hi, np.uint32, hi, dup=True), np.full(n, 7, np.uint32),
-             np.arange(n, dtype=np.uint32), np.full(n, 0xFFFFFFFF, np.uint32)]
-    inter = np.arange(n, dtype=np.uint32)  # run r holds r, r+K, r+2K, ... of its group
+    top = np.iinfo(dt).max
+    cases = [runs_input(n, hi, dt, hi, dup=True), np.full(n, 7, dt), np.arange(n, dtype=dt), np.full(n, top, dt)]
+    inter = np.arange(n, dtype=dt)  # run r holds r, r+K, r+2K, ... of its group
     w = 1 << hi
     for g in range(0, n, K * w):
         for r in range(K):
             seg = inter[g + r * w: g + (r + 1) * w]
-            seg[:] = np.arange(seg.size, dtype=np.uint32) * K + r
+            seg[:] = np.arange(seg.size, dtype=dt) * K + r
     cases.append(inter)
+    if dt == np.uint64:
+        cases.append((inter << np.uint64(32)) | np.uint64(5))
+        hiw = inter.copy()  # run r: keys r << 32 .. with equal low words: only the high word orders them
+        for g in range(0, n, K * w):
+            for r in range(K):
+                seg = hiw[g + r * w: g + (r + 1) * w]
+                seg[:] = (np.arange(seg.size, dtype=np.uint64) // 3 * K + r) << np.uint64(32)
+        cases.append(hiw)
     for x in cases:
         np.testing.assert_array_equal(run_level(ctx, x, hi, "run_mergek", lk), expectk(x, hi, lk))
 
@@ -135,6 +148,10 @@ def test_merge_level_rejects_bad_shapes(ctx):
     for hi, lk in ((11, 2), (14, 2), (15, 5)):  # multi-way: runs shorter than a SORT tile; lk > 4
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi, "run_mergek", lk)
+    x64 = np.arange(1 << 16, dtype=np.uint64)
+    for hi, lk in ((12, 2), (13, 5)):  # u64: runs shorter than the 2^13 SORT tile; lk > 4
+        with pytest.raises(misort.MisortError):
+            run_level(ctx, x64, hi, "run_mergek", lk)
 
 
 CHILD = r"""
@@ -188,6 +205,10 @@ ctx.close()
     (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 21) + 4099),
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_IT": "32"}, (1 << 20) + 5),
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_NT": "512"}, (1 << 20) + 5),
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "0"}, (1 << 21) + 4099),  # 2-way passes
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "2"}, (1 << 21) + 4099),
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "4"}, (1 << 22) + 3),
+    (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 25) + 12345),  # chained 8-way passes, u128 fence merges
 ])
 def test_full_sort_merge_from(kb, env, n):
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
@@ -197,8 +218,8 @@ def test_full_sort_merge_from(kb, env, n):
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
     _, count, _, countk, verdict = line.split()
     assert verdict == "OK", line
-    cap = int(env.get("MISORT_MULTIWAY", "3"))
-    if kb == 4 and cap >= 2 and int(count) >= 2:
+    cap = int(env.get("MISORT_MULTIWAY" if kb == 4 else "MISORT_MULTIWAY_U64", "3"))
+    if cap >= 2 and int(count) >= 2:
         assert int(countk) == -(-int(count) // cap)  # the fewest multi-way passes
     else:
         assert int(countk) == 0

@@ -136,8 +136,14 @@ def test_plan_pass_counts():
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
     assert len(misort.plan(1 << 24, 4)) == 15  # cache-resident u32 sizes stay on the network
-    # u64: 2^13-key SORT tiles, then merge levels
-    assert len(misort.plan((1 << 29) - 3, 8)) == 1 + 29 - 13
+    # u64: 2^13-key SORT tiles, then 16 levels in six multi-way passes
+    # (128-bit fences; 2-way passes would be 1 + 16)
+    p29 = misort.plan((1 << 29) - 3, 8)
+    assert p29[0][0] == KIND_SORT and [q[0] for q in p29[1:]] == [KIND_RUNSK] * 6
+    assert [q[2] for q in p29[1:]] == [3, 3, 3, 3, 2, 2]
+    # a u64 multi-way pass ends at 2^29 at most (32-bit row offsets of 8-byte keys)
+    assert [q[0] for q in misort.plan(1 << 30, 8)] == [KIND_SORT] + [KIND_RUNSK] * 6 + [KIND_RUNS]
+    assert [q[0] for q in misort.plan(1 << 14, 8)] == [KIND_SORT, KIND_RUNS]  # one level: 2-way
 
 
 @pytest.mark.parametrize("key_bytes", [4, 8])
