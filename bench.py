@@ -408,8 +408,8 @@ def main(argv=None):
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys), then merge passes: u32 up to 3 "
-                      "levels per HBM pass (8-way, runsk.hip), u64 one level per pass "
+        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys), then multi-way merge passes: up to 3 "
+                      "merge levels per HBM pass (8-way, runsk.hip; u64 with 128-bit fences) "
                       "(the reference's local std::sort, psort.cc:175)")
         out = {
             "metric": METRIC,

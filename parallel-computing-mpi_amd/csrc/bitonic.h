@@ -691,9 +691,13 @@ __host__ __device__ constexpr bool pgroup_rep(int k, int cnt, int top, bool flip
 // LDS -> registers (final slot window SF, mirrored upper slots if MF) -> the
 // pass's last register stages -> HBM.  Slots are handled one stage-connected
 // group at a time, so only 2^CNT vectors are live.
+// fence (SORT tiles of u32 keys only, may be null): the first multi-way merge
+// pass's fences, written here instead of gathered from HBM by k_fence_gather
+// -- the key at every 2^MERGEK_FENCE_LOG2-th position of the sorted tile,
+// packed as runsk.hip's fpack does for runs of 2^LT keys in groups of 2^flk.
 template <typename K, int LT, int MODE, int SF, bool MF, int TOP, int CNT, bool FLIP, bool COMP>
 __device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m, int64_t tile, int64_t n,
-                                            bool full, int t) {
+                                            bool full, int t, uint64_t* fence = nullptr, int flk = 0) {
     typedef TileGeo<K, LT> G;
     constexpr int NG = 1 << CNT;
 #pragma unroll
@@ -735,7 +739,17 @@ __device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m
             K x[G::V];
 #pragma unroll
             for (int j = 0; j < G::V; ++j) x[j] = mk ? w[S][G::V - 1 - j] : w[S][j];
-            store_slot<K, LT, MODE>(out, m, tile, n, full, place<K, LT, SF>(k, slot_lane<K, LT, MF>(k, t)), x);
+            const int e = place<K, LT, SF>(k, slot_lane<K, LT, MF>(k, t));
+            store_slot<K, LT, MODE>(out, m, tile, n, full, e, x);
+            if constexpr (MODE == TM_SORT && sizeof(K) == 4) {
+                constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
+                const int64_t gi = (tile << LT) + e;
+                if (fence && (e & FGM) == 0 && gi < n)
+                    fence[gi >> MERGEK_FENCE_LOG2] =
+                        ((uint64_t)x[0] << 32) |
+                        ((uint64_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
+                        (uint64_t)((e & ((1 << LT) - 1)) >> MERGEK_FENCE_LOG2);
+            }
         }
     }
 }
@@ -989,7 +1003,7 @@ __device__ __forceinline__ void tile_merge_levels(uint32_t* s, int t) {
 
 template <bool PERSIST, bool FULL>
 __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, TileMap m,
-                                                      int64_t tile0) {
+                                                      int64_t tile0, uint64_t* fence, int flk) {
     typedef uint32_t K;
     constexpr int LT = 15;
     typedef TileGeo<K, LT> G;
@@ -1043,13 +1057,15 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
             sort_levels_w<K, WL + 1, MISORT_SORT_TOP>(s, t);
         }
         final_store<K, LT, TM_SORT, SL, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n, FULL,
-                                                                                         t);
+                                                                                         t, fence, flk);
         if constexpr (!PERSIST) break;
         __syncthreads();
     }
 }
 
-inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+// fence/flk: see final_store (null: no fences).
+inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
+                            int flk = 0) {
     static int64_t cap = 0;
     TileMap m{};
     const int64_t nfull = n >> 15;
@@ -1065,12 +1081,12 @@ inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStr
         m.ntiles = nfull;
         const int64_t want = persist ? cap * plan_knobs().grid_mult : nfull;
         const int64_t grid = nfull < want ? nfull : want;
-        if (persist) k_sort_u32<true, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0);
-        else k_sort_u32<false, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0);
+        if (persist) k_sort_u32<true, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0, fence, flk);
+        else k_sort_u32<false, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, m, 0, fence, flk);
     }
     if ((nfull << 15) < n) {
         m.ntiles = nfull + 1;
-        k_sort_u32<false, false><<<1, 1024, 0, s>>>(in, out, n, m, nfull);
+        k_sort_u32<false, false><<<1, 1024, 0, s>>>(in, out, n, m, nfull, fence, flk);
     }
 }
 
@@ -1410,9 +1426,13 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
     return plan(k, LT, rmax, cmin, kn.span && LT == LTR, G::KB, G::VB, (int)sizeof(K), wide);
 }
 
+// The u32 SORT pass runs k_sort_u32 (launch_pass's condition).
+inline bool sort_u32_path() { return MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 10 && plan_knobs().sort_u32; }
+
 // One pass of a plan over n keys, src -> dst.
 template <typename K, int LT, int LTR>
-void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hipStream_t s) {
+void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hipStream_t s,
+                 uint64_t* fence = nullptr, int flk = 0) {
     TileMap tm{};
     tm.ntiles = (n + (1 << LT) - 1) >> LT;
     if (p.kind == KIND_TILE_SORT) {
@@ -1420,7 +1440,7 @@ void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hi
             if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
             else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
         } else if (LT == 15 && MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 10 && plan_knobs().sort_u32) {
-            launch_sort_u32(src, dst, n, s);
+            launch_sort_u32(src, dst, n, s, fence, flk);
         } else {
             launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
         }
@@ -1446,13 +1466,17 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
     int fence_phase = 0;  // multi-way passes: fence buffer holding the next pass's fences
+    // the u32 SORT pass writes the first multi-way pass's fences (no gather pass)
+    const bool sort_fences = sizeof(K) == 4 && LT == 15 && np > 1 && ps[0].kind == KIND_TILE_SORT &&
+                             ps[1].kind == KIND_RUNSK && ps[1].hi == LT && sort_u32_path() &&
+                             !(io && io->before_first);
     for (int i = 0; i < np; ++i) {
         // ping-pong: pass i writes `out` iff an even number of passes follow it
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
         const Pass& p = ps[i];
         HookScope hs(hook, p.kind, bytes, s);
         if (p.kind == KIND_RUNSK) {
-            const bool prevk = i > 0 && ps[i - 1].kind == KIND_RUNSK;
+            const bool prevk = i > 0 && (ps[i - 1].kind == KIND_RUNSK || (i == 1 && sort_fences));
             const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
             const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next);
             if (e != hipSuccess) return e;
@@ -1482,6 +1506,10 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
         } else if (runs) {
             const hipError_t e = merge_level<K>(src, dst, n, p.hi, s);
             if (e != hipSuccess) return e;
+        } else if (i == 0 && sort_fences) {
+            uint64_t* f = (uint64_t*)mergek_fence_buffer(n, (int)sizeof(K), 0, s);
+            if (!f) return hipErrorOutOfMemory;
+            launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s, f, ps[1].R);
         } else {
             launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s);
         }

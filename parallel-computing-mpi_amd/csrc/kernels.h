@@ -98,6 +98,15 @@ hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, i
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next);
 int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
+// Fence stride of the multi-way passes (log2 keys).
+#ifndef MISORT_MK_FG_LOG2
+#define MISORT_MK_FG_LOG2 7
+#endif
+constexpr int MERGEK_FENCE_LOG2 = MISORT_MK_FG_LOG2;
+// The per-stream fence buffer `phase` of a multi-way pass over n keys (the
+// one merge_levelk reads with that phase), for a SORT pass that writes the
+// first pass's fences itself; null on allocation failure.
+void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s);
 int merge_levelk_lw_min(int key_bytes);   // shortest input runs (log2) of a multi-way pass
 int merge_levelk_lwk_max(int key_bytes);  // largest output runs (log2)
 

@@ -45,10 +45,7 @@
 namespace misort {
 namespace {
 
-#ifndef MISORT_MK_FG_LOG2
-#define MISORT_MK_FG_LOG2 7
-#endif
-constexpr int FG_LOG2 = MISORT_MK_FG_LOG2;
+constexpr int FG_LOG2 = MERGEK_FENCE_LOG2;  // kernels.h (the u32 SORT pass writes fences too)
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
 #ifndef MISORT_MK_NT
 #define MISORT_MK_NT 512
@@ -900,6 +897,13 @@ hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, i
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next) {
     return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next);
+}
+void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
+    // the sizes merge_pass computes, so the buffer never moves between the two
+    const int64_t nf = (n + FG - 1) >> FG_LOG2;
+    const size_t fb = ((size_t)nf * (key_bytes == 8 ? sizeof(u128) : sizeof(uint64_t)) + 255) & ~(size_t)255;
+    char* fbase = (char*)scratch(0, 2 * fb, s);
+    return fbase ? fbase + (phase & 1) * fb : nullptr;
 }
 int merge_levelk_lw_min(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LW_MIN : KTr<uint32_t>::LW_MIN; }
 int merge_levelk_lwk_max(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LWK_MAX : KTr<uint32_t>::LWK_MAX; }
