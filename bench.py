@@ -214,13 +214,15 @@ def port_baseline(logn, why):
             "fallback_reason": why}
 
 
-def load_traffic():
-    """Per-launch HBM bytes from committed rocprofv3 --pmc summaries (or None)."""
-    p = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        return json.load(f)
+def load_traffic(workload=None):
+    """Per-launch HBM bytes from committed rocprofv3 --pmc summaries (or None):
+    profiles/traffic_<workload>.json if present, else profiles/traffic.json."""
+    for name in ([f"traffic_{workload}.json"] if workload else []) + ["traffic.json"]:
+        p = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(p):
+            with open(p) as f:
+                return json.load(f)
+    return None
 
 
 # -------------------------------------------------------------------- ranks
@@ -456,9 +458,9 @@ def main(argv=None):
             hbm = {k: v for k, v in kern.items() if k != "exchange"}
             dom = max(hbm.items(), key=lambda kv: kv[1][1])
             name, (nl, tms, byt) = dom
-            traffic = load_traffic()
-            tr = None
             wl = f"{args.dtype}_2e{args.logn}_n{nranks}"
+            traffic = load_traffic(wl)
+            tr = None
             if traffic and traffic.get("workload") == wl and name in traffic and \
                     traffic[name].get("bytes_per_launch"):
                 tr = traffic[name]["bytes_per_launch"]

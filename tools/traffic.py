@@ -29,7 +29,8 @@ import sys
 FAMILY = {"0": "tile_sort", "1": "tile_merge", "2": "global_pass", "3": "span_pass"}
 root = sys.argv[1]
 # u32 sorts: k_runs_* on unsigned long are the multi-way passes' fence merges;
-# u64 sorts: they are the sort's own merge levels
+# u64 sorts: they are the sort's own 2-way merge levels, and k_runs_* on
+# unsigned __int128 the fence merges
 U32 = not (os.environ.get("WORKLOAD") or "").startswith("u64")
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
@@ -42,8 +43,8 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
             fam = "tile_sort"
         elif "k_rows_wide" in name:
             fam = "wide_pass"
-        elif U32 and re.search(r"k_runs_\w+<unsigned long", name):
-            fam = "runk_plan"  # the 64-bit fence merges of a multi-way pass (u32 sorts)
+        elif (U32 and re.search(r"k_runs_\w+<unsigned long", name)) or re.search(r"k_runs_\w+<unsigned __int128", name):
+            fam = "runk_plan"  # the fence merges of a multi-way pass (u64 fences: u32 sorts; u128: u64 sorts)
         elif "k_runs_merge" in name:
             fam = "run_merge_kernel"
         elif "k_runs_partition" in name:
