@@ -112,9 +112,12 @@ int64_t misort_block_size(int64_t n, int p, int rank);
  * together), and max_size <= 0 means the largest block.  Steps: local sort
  * (psort.cc:175) then d(d+1)/2 rounds of RCCL send/recv with the partner plus a
  * device merge-split.  At P = 1 everything is enqueued on `stream`; at P > 1
- * the host waits on the stream at the start (size exchange) and 1-3 times per
- * stage (splitter samples to the host, and for delta-coded messages the coded
- * size and the size handshake), the rest is enqueued. */
+ * the host waits on the stream at the start (size exchange) and once per
+ * stage: the exchange count k is computed on the device from the swapped
+ * splitter samples, the encoder takes it from device memory, and the ranks'
+ * (coded, raw) message sizes -- which carry k -- are exchanged from device
+ * memory; the host reads them once to size the RCCL send/recv.  Without the
+ * codec (MISORT_COMPRESS=0) k is computed on the host: two waits per stage. */
 int misort_parallel_bitonic_sort(misort_ctx* ctx, int dtype, void* d_keys, int64_t loc_size,
                                  int64_t max_size, void* stream);
 /* Same, out of place: d_in is left unchanged, d_out receives the block
@@ -136,9 +139,6 @@ int misort_parallel_bitonic_sort_oop(misort_ctx* ctx, int dtype, const void* d_i
 int misort_local_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out, int64_t n,
                       void* stream);
 
-/* Device half of compare_split_{max,min} (psort.cc:116-164) without the
- * exchange: d_out[0..nloc) = the nloc largest (keep_max=1) or smallest
- * (keep_max=0) keys of the sorted blocks local U recv, ascending. */
 /* psort.cc:377-490 parallel_quick_sort (the reference binary's shipped sort,
  * called at psort.cc:647-648): d rounds of median-of-medians pivoting over
  * shrinking hypercube sub-groups, RCCL send/recv with the partner, device merge.
@@ -160,6 +160,9 @@ int misort_parallel_quick_sort(misort_ctx* ctx, int dtype, const void* d_in, int
 int misort_parallel_sample_sort(misort_ctx* ctx, int dtype, const void* d_in, void* d_out,
                                 int64_t loc_size, int64_t max_size, void* stream);
 
+/* Device half of compare_split_{max,min} (psort.cc:116-164) without the
+ * exchange: d_out[0..nloc) = the nloc largest (keep_max=1) or smallest
+ * (keep_max=0) keys of the sorted blocks local U recv, ascending. */
 int misort_merge_split(misort_ctx* ctx, int dtype, const void* d_local, int64_t nloc,
                        const void* d_recv, int64_t nrecv, void* d_out, int keep_max,
                        void* stream);

@@ -12,8 +12,15 @@
 //
 // Stream (u32 words): nblk headers of 4 words {base lo, base hi, payload
 // offset (words, from the stream start), width}, then the payloads.
+//
+// The run to encode is given on the device as {offset, count} with an upper
+// bound on the count on the host: the compare-split stage computes its
+// exchange count on the device, and the host learns it together with the
+// coded size in the stage's one size exchange.  The payload offsets are an
+// exclusive scan of the per-block word counts -- chunks of SCN blocks scanned
+// in LDS (k_scan_words), then the chunk totals (k_scan_chunks); no library
+// scan.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
 
@@ -21,18 +28,29 @@ namespace misort {
 namespace {
 
 constexpr int CB = 1024, CT = 256, CI = CB / CT;  // keys per block, threads, keys per thread
+constexpr int SCN = 1024;                         // blocks per chunk of the payload-offset scan
 
 __device__ __forceinline__ int width_of(uint64_t d) { return d ? 64 - __builtin_clzll(d) : 0; }
 
 // Per block: payload words for its gaps at the block's width.  (Lane-strided
 // loads of 4 consecutive keys; measured faster here than coalesced loads with a
-// cross-lane predecessor, and than packing through LDS atomics.)
+// cross-lane predecessor, and than packing through LDS atomics.)  The run is
+// base + run[0] .. + run[1] keys; blocks past its end write no words.
 template <typename K>
-__global__ __launch_bounds__(CT) void k_codec_width(const K* __restrict__ keys, int64_t n,
+__global__ __launch_bounds__(CT) void k_codec_width(const K* __restrict__ base, const int64_t* __restrict__ run,
                                                     uint32_t* __restrict__ words, uint8_t* __restrict__ wid) {
     __shared__ uint64_t red[CT / 64];
     const int64_t b = blockIdx.x, k0 = b * CB;
     const int t = threadIdx.x;
+    const int64_t n = run[1];
+    const K* __restrict__ keys = base + run[0];
+    if (k0 >= n) {
+        if (t == 0) {
+            words[b] = 0;
+            wid[b] = 0;
+        }
+        return;
+    }
     uint64_t mx = 0;
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
@@ -51,12 +69,72 @@ __global__ __launch_bounds__(CT) void k_codec_width(const K* __restrict__ keys, 
     }
 }
 
+// Inclusive scan of v over the SCN lanes of the block (16 waves of 64).
+__device__ __forceinline__ uint32_t scan_block(uint32_t v, uint32_t* sw) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o, 64);
+        v += lane >= o ? u : 0u;
+    }
+    if (lane == 63) sw[wv] = v;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int q = 0; q < wv; ++q) pre += sw[q];
+    __syncthreads();
+    return v + pre;
+}
+
+// Chunk c of SCN blocks: off[b] = the words of the chunk's blocks before b
+// (chunk-local exclusive scan), csum[c] = the chunk's total.
+__global__ __launch_bounds__(SCN) void k_scan_words(const uint32_t* __restrict__ words, int64_t nb,
+                                                    uint32_t* __restrict__ off, uint32_t* __restrict__ csum) {
+    __shared__ uint32_t sw[SCN / 64];
+    const int64_t b = (int64_t)blockIdx.x * SCN + threadIdx.x;
+    const uint32_t v = b < nb ? words[b] : 0u;
+    const uint32_t inc = scan_block(v, sw);
+    if (b < nb) off[b] = inc - v;
+    if (threadIdx.x == SCN - 1) csum[blockIdx.x] = inc;
+}
+
+// One workgroup: the chunk totals exclusive-scanned in place (carried over
+// rounds of SCN), then the message sizes sizes[0] = coded words (4 header
+// words per block + the payload words), sizes[1] = raw words (count * key
+// words) of the run's count run[1].
+__global__ __launch_bounds__(SCN) void k_scan_chunks(uint32_t* __restrict__ csum, int64_t nc,
+                                                     const int64_t* __restrict__ run, int key_words,
+                                                     int64_t* __restrict__ sizes) {
+    __shared__ uint32_t sw[SCN / 64];
+    __shared__ uint32_t tot;
+    uint32_t carry = 0;
+    for (int64_t c0 = 0; c0 < nc; c0 += SCN) {
+        const int64_t c = c0 + threadIdx.x;
+        const uint32_t v = c < nc ? csum[c] : 0u;
+        const uint32_t inc = scan_block(v, sw);
+        if (c < nc) csum[c] = carry + inc - v;
+        if (threadIdx.x == SCN - 1) tot = inc;
+        __syncthreads();
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int64_t n = run[1];
+        const int64_t nb = (n + CB - 1) / CB;
+        sizes[0] = n > 0 ? 4 * nb + (int64_t)carry : 0;
+        sizes[1] = n * key_words;
+    }
+}
+
 template <typename K>
-__global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ keys, int64_t n, int64_t nblk,
-                                                   const uint32_t* __restrict__ off, const uint8_t* __restrict__ wid,
-                                                   uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ kbase, const int64_t* __restrict__ run,
+                                                   const uint32_t* __restrict__ off, const uint32_t* __restrict__ coff,
+                                                   const uint8_t* __restrict__ wid, uint32_t* __restrict__ out) {
     __shared__ uint64_t gap[CB];
     const int64_t b = blockIdx.x, k0 = b * CB;
+    const int64_t n = run[1];
+    if (k0 >= n) return;
+    const K* __restrict__ keys = kbase + run[0];
+    const int64_t nblk = (n + CB - 1) / CB;
     const int t = threadIdx.x;
     const int64_t cnt = n - k0 < CB ? n - k0 : CB;
 #pragma unroll
@@ -66,7 +144,7 @@ __global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ keys, i
     }
     __syncthreads();
     const int w = wid[b];
-    const uint32_t base_w = (uint32_t)(4 * nblk) + off[b];
+    const uint32_t base_w = (uint32_t)(4 * nblk) + off[b] + coff[b / SCN];
     const int nw = (int)(((cnt - 1) * w + 31) >> 5);
     if (t == 0) {
         const uint64_t base = (uint64_t)keys[k0];
@@ -89,8 +167,9 @@ __global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ keys, i
     }
 }
 
-__global__ void k_codec_total(const uint32_t* off, const uint32_t* words, int64_t nb, uint32_t* total) {
-    *total = (uint32_t)(4 * nb) + off[nb - 1] + words[nb - 1];
+__global__ void k_set_run(int64_t* run, int64_t offset, int64_t n) {
+    run[0] = offset;
+    run[1] = n;
 }
 
 // Lane t rebuilds keys 4t..4t+3 of its block: key p = base + the gaps before
@@ -163,34 +242,45 @@ __global__ __launch_bounds__(CT) void k_codec_unpack(const uint32_t* __restrict_
 
 int64_t codec_blocks(int64_t n) { return (n + CB - 1) / CB; }
 
-size_t codec_scratch_bytes(int64_t n) {
+// words, off, wid per block and the chunk totals
+static size_t arrays_bytes(int64_t n) {
     const int64_t nb = codec_blocks(n) > 0 ? codec_blocks(n) : 1;
-    size_t tmp = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)nb);
-    return (size_t)nb * (2 * sizeof(uint32_t) + 1) + 512 + tmp;
+    const int64_t nc = (nb + SCN - 1) / SCN;
+    return (size_t)nb * (2 * sizeof(uint32_t) + 1) + (size_t)nc * sizeof(uint32_t);
 }
+// + 256 for alignment, + the {offset, count} slot codec_encode keeps at the end
+size_t codec_scratch_bytes(int64_t n) { return arrays_bytes(n) + 512; }
 
 int64_t codec_max_words(int64_t n, int key_bytes) {
     return 4 * codec_blocks(n) + (n * key_bytes * 8 + 31) / 32 + codec_blocks(n);
 }
 
 template <typename K>
-hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, size_t scratch_bytes,
-                        uint32_t* d_total, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int64_t nb = codec_blocks(n);
-    char* p = (char*)scratch;
+hipError_t codec_encode_dev(const K* base, const int64_t* run, int64_t n_max, uint32_t* out, void* scratch,
+                            size_t scratch_bytes, int64_t* sizes, hipStream_t s) {
+    const int64_t nb = codec_blocks(n_max) > 0 ? codec_blocks(n_max) : 1;
+    const int64_t nc = (nb + SCN - 1) / SCN;
+    if (scratch_bytes < arrays_bytes(n_max) + 256) return hipErrorInvalidValue;
+    char* p = (char*)(((uintptr_t)scratch + 255) & ~(uintptr_t)255);
     uint32_t* words = (uint32_t*)p;
     uint32_t* off = words + nb;
-    uint8_t* wid = (uint8_t*)(off + nb);
-    void* tmp = (void*)(((uintptr_t)(wid + nb) + 255) & ~(uintptr_t)255);
-    size_t tmp_bytes = scratch_bytes - (size_t)((char*)tmp - p);
-    k_codec_width<K><<<(unsigned)nb, CT, 0, s>>>(keys, n, words, wid);
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, words, off, (int)nb, s);
-    if (e != hipSuccess) return e;
-    k_codec_pack<K><<<(unsigned)nb, CT, 0, s>>>(keys, n, nb, off, wid, out);
-    k_codec_total<<<1, 1, 0, s>>>(off, words, nb, d_total);
+    uint32_t* csum = off + nb;
+    uint8_t* wid = (uint8_t*)(csum + nc);
+    k_codec_width<K><<<(unsigned)nb, CT, 0, s>>>(base, run, words, wid);
+    k_scan_words<<<(unsigned)nc, SCN, 0, s>>>(words, nb, off, csum);
+    k_scan_chunks<<<1, SCN, 0, s>>>(csum, nc, run, (int)(sizeof(K) / 4), sizes);
+    k_codec_pack<K><<<(unsigned)nb, CT, 0, s>>>(base, run, off, csum, wid, out);
     return hipGetLastError();
+}
+
+template <typename K>
+hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, size_t scratch_bytes,
+                        int64_t* sizes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    // the {offset, count} slot at the end of the scratch
+    int64_t* run = (int64_t*)(((uintptr_t)scratch + scratch_bytes - 64) & ~(uintptr_t)15);
+    k_set_run<<<1, 1, 0, s>>>(run, 0, n);
+    return codec_encode_dev<K>(keys, run, n, out, scratch, (size_t)((char*)run - (char*)scratch), sizes, s);
 }
 
 template <typename K>
@@ -200,9 +290,13 @@ hipError_t codec_decode(const uint32_t* in, int64_t n, K* keys, hipStream_t s) {
     return hipGetLastError();
 }
 
-template hipError_t codec_encode<uint32_t>(const uint32_t*, int64_t, uint32_t*, void*, size_t, uint32_t*,
+template hipError_t codec_encode_dev<uint32_t>(const uint32_t*, const int64_t*, int64_t, uint32_t*, void*, size_t,
+                                               int64_t*, hipStream_t);
+template hipError_t codec_encode_dev<uint64_t>(const uint64_t*, const int64_t*, int64_t, uint32_t*, void*, size_t,
+                                               int64_t*, hipStream_t);
+template hipError_t codec_encode<uint32_t>(const uint32_t*, int64_t, uint32_t*, void*, size_t, int64_t*,
                                            hipStream_t);
-template hipError_t codec_encode<uint64_t>(const uint64_t*, int64_t, uint32_t*, void*, size_t, uint32_t*,
+template hipError_t codec_encode<uint64_t>(const uint64_t*, int64_t, uint32_t*, void*, size_t, int64_t*,
                                            hipStream_t);
 template hipError_t codec_decode<uint32_t>(const uint32_t*, int64_t, uint32_t*, hipStream_t);
 template hipError_t codec_decode<uint64_t>(const uint32_t*, int64_t, uint64_t*, hipStream_t);

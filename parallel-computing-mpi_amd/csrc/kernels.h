@@ -130,6 +130,14 @@ hipError_t count_descents(const T* a, int64_t n, unsigned long long* count, hipS
 template <typename K>
 hipError_t gather_samples(const K* a, int64_t n, int64_t stride, K* out, int64_t count, hipStream_t s);
 
+// The compare-split bracket on the device: from the partners' samples (sa of
+// the keep-min side's na keys, sb of the keep-max side's nb keys, as
+// gather_samples takes them) run[0..1] = {send offset, k} of this rank's
+// message (keep_max: its bottom k keys; else its top k of nloc).
+template <typename K>
+hipError_t exchange_count(const K* sa, int64_t na, const K* sb, int64_t nb, int keep_max, int64_t nloc,
+                          int64_t* run, hipStream_t s);
+
 // IEEE double bits <-> order-preserving u64, in place.
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s);
 hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s);
@@ -141,14 +149,19 @@ hipError_t fill_splitmix_u64(uint64_t* out, int64_t n, uint64_t seed, int64_t g0
 // Lossless delta coding of a sorted run (codec.hip), for the compare-split
 // exchange: blocks of 1024 keys, first key + gaps packed at the block's width.
 // codec_encode writes the stream to `out` (<= codec_max_words(n) u32 words)
-// and its length in words to *d_total (device); scratch holds
-// codec_scratch_bytes(n) bytes.  codec_decode restores the n keys.
+// and sizes[0..1] = {coded words, raw words} (device int64); scratch holds
+// codec_scratch_bytes(n) bytes.  codec_encode_dev does the same for the run
+// base + run[0] of run[1] keys, both device int64, run[1] <= n_max.
+// codec_decode restores the n keys.
 int64_t codec_blocks(int64_t n);
 size_t codec_scratch_bytes(int64_t n);
 int64_t codec_max_words(int64_t n, int key_bytes);
 template <typename K>
 hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, size_t scratch_bytes,
-                        uint32_t* d_total, hipStream_t s);
+                        int64_t* sizes, hipStream_t s);
+template <typename K>
+hipError_t codec_encode_dev(const K* base, const int64_t* run, int64_t n_max, uint32_t* out, void* scratch,
+                            size_t scratch_bytes, int64_t* sizes, hipStream_t s);
 template <typename K>
 hipError_t codec_decode(const uint32_t* in, int64_t n, K* keys, hipStream_t s);
 

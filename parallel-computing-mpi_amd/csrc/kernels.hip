@@ -183,6 +183,53 @@ __global__ void k_gather_samples(const K* __restrict__ a, int64_t n, int64_t str
     out[c] = a[x];
 }
 
+// The compare-split bracket on the device (runtime.cpp corank_lower, same
+// predicate, same answer): i_lo = the first i in [max(0, na-nb), na] whose
+// "A[i] <= B[na-1-i]" is not certain from the samples (sa: samples of A's na
+// keys, sb: of B's nb keys, stride max(256, ceil(n/32768)), the last sample
+// index clamped).  The predicate is true then false, so one workgroup narrows
+// [lo, hi] by EXN points per round instead of one bisection step per load.
+// run = {send offset, k}: k = na - i_lo keys each side sends, from offset 0
+// (the keep-max side sends its bottom k) or nloc - k (the keep-min side its top k).
+constexpr int EXN = 1024;
+inline int64_t dev_sample_stride_host(int64_t n) { return std::max<int64_t>(256, (n + 32767) / 32768); }
+__device__ __forceinline__ int64_t dev_sample_stride(int64_t n) {
+    const int64_t s = (n + 32767) / 32768;
+    return s > 256 ? s : 256;
+}
+template <typename K>
+__global__ __launch_bounds__(EXN) void k_exchange_count(const K* __restrict__ sa, int64_t ca, int64_t na,
+                                                        const K* __restrict__ sb, int64_t cb, int64_t nb, int mx,
+                                                        int64_t nloc, int64_t* __restrict__ run) {
+    const int64_t Sa = dev_sample_stride(na), Sb = dev_sample_stride(nb);
+    auto certain = [&](int64_t i) {  // A[i] <= B[na-1-i] from the samples
+        const int64_t ia = i / Sa + 1 < ca - 1 ? i / Sa + 1 : ca - 1;
+        const int64_t jb = (na - 1 - i) / Sb < cb - 1 ? (na - 1 - i) / Sb : cb - 1;
+        return sa[ia] <= sb[jb];
+    };
+    int64_t lo = na > nb ? na - nb : 0, hi = na;
+    if (na == 0) lo = hi = 0;
+    else if (nb == 0) lo = hi = na;
+    while (lo < hi) {
+        const int64_t step = (hi - lo + EXN - 1) / EXN;
+        const int64_t x = lo + (int64_t)threadIdx.x * step;
+        const int c = __syncthreads_count(x < hi && certain(x));  // a prefix of the points
+        if (step == 1) {
+            lo += c;
+            break;
+        }
+        const int64_t nlo = c > 0 ? lo + (int64_t)(c - 1) * step + 1 : lo;
+        const int64_t xc = lo + (int64_t)c * step;
+        hi = xc < hi ? xc : hi;
+        lo = nlo;
+    }
+    if (threadIdx.x == 0) {
+        const int64_t k = na - lo;
+        run[0] = mx ? 0 : nloc - k;
+        run[1] = k;
+    }
+}
+
 // psort.cc:88-101: first index i in [0, n) with x <= a[i] (n if none), one lane.
 template <typename K>
 __global__ void k_lower_bound(const K* __restrict__ a, int64_t n, K x, int64_t* __restrict__ out) {
@@ -302,6 +349,19 @@ hipError_t gather_samples(const K* a, int64_t n, int64_t stride, K* out, int64_t
 }
 template hipError_t gather_samples<uint32_t>(const uint32_t*, int64_t, int64_t, uint32_t*, int64_t, hipStream_t);
 template hipError_t gather_samples<uint64_t>(const uint64_t*, int64_t, int64_t, uint64_t*, int64_t, hipStream_t);
+
+template <typename K>
+hipError_t exchange_count(const K* sa, int64_t na, const K* sb, int64_t nb, int keep_max, int64_t nloc,
+                          int64_t* run, hipStream_t s) {
+    const int64_t ca = na > 0 ? (na + dev_sample_stride_host(na) - 1) / dev_sample_stride_host(na) + 1 : 0;
+    const int64_t cb = nb > 0 ? (nb + dev_sample_stride_host(nb) - 1) / dev_sample_stride_host(nb) + 1 : 0;
+    k_exchange_count<K><<<1, EXN, 0, s>>>(sa, ca, na, sb, cb, nb, keep_max, nloc, run);
+    return hipGetLastError();
+}
+template hipError_t exchange_count<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int64_t, int, int64_t,
+                                             int64_t*, hipStream_t);
+template hipError_t exchange_count<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t, int, int64_t,
+                                             int64_t*, hipStream_t);
 
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;

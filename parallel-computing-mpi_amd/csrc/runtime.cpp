@@ -622,33 +622,32 @@ int relay_raw(misort_ctx* c, int bit, const void* sbuf, size_t bytes, void* rbuf
     return relay_exchange(c, 4, bit, sbuf, bytes, rbuf, rbytes, s, nullptr, &units);
 }
 
-// One compare-split message exchange of k sorted keys each way, delta-coded
-// (codec.hip).  *rkeys receives the partner's k keys (decoded into c->recv, or
+// One compare-split message exchange, delta-coded (codec.hip), with the
+// exchange count k computed on the device: run = {send offset, k} (device,
+// from exchange_count) into `base`, k <= kmax.  The encoder takes the run from
+// device memory, the ranks exchange their (coded words, raw words) pairs
+// straight from device memory, and one host sync serves the count, the
+// coded-or-raw choice and the sizes -- the host never waits for k alone.
+// *k_out = k (0: nothing crossed; the relay still ran, others may pass through
+// this rank); *rkeys receives the partner's k keys (decoded into c->recv, or
 // the raw message in c->enc_recv when the partner sent it uncoded).
-int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sbuf, int64_t k, const void** rkeys,
-                   hipStream_t s) {
+int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* base, int64_t nloc, bool keep_max,
+                   const int64_t* run, int64_t kmax, int64_t* k_out, const void** rkeys, hipStream_t s) {
     const size_t w = key_bytes(dtype);
-    const int64_t raw_words = k * (int64_t)w / 4, maxw = misort::codec_max_words(k, (int)w);
+    const int64_t maxw = misort::codec_max_words(kmax, (int)w), raw_max = kmax * (int64_t)w / 4;
     int rc;
-    if ((rc = c->enc_send.ensure((size_t)maxw * 4))) return rc;
-    if ((rc = c->enc_recv.ensure((size_t)std::max(maxw, raw_words) * 4))) return rc;
-    const size_t scr = misort::codec_scratch_bytes(k) + 64;
+    if ((rc = c->enc_send.ensure((size_t)std::max<int64_t>(maxw, 4) * 4))) return rc;
+    if ((rc = c->enc_recv.ensure((size_t)std::max<int64_t>(std::max(maxw, raw_max), 4) * 4))) return rc;
+    const size_t scr = misort::codec_scratch_bytes(kmax) + 64;
     if ((rc = c->codec_scr.ensure(scr))) return rc;
-    if ((rc = c->small.ensure(64))) return rc;
-    uint32_t* d_total = (uint32_t*)c->small.p;
-    hipError_t e = w == 4 ? misort::codec_encode<uint32_t>((const uint32_t*)sbuf, k, (uint32_t*)c->enc_send.p,
-                                                           c->codec_scr.p, scr, d_total, s)
-                          : misort::codec_encode<uint64_t>((const uint64_t*)sbuf, k, (uint32_t*)c->enc_send.p,
-                                                           c->codec_scr.p, scr, d_total, s);
+    int64_t* d_sz = (int64_t*)c->small.p;  // [coded words, raw words] mine, then the partner's
+    hipError_t e = w == 4 ? misort::codec_encode_dev<uint32_t>((const uint32_t*)base, run, kmax,
+                                                               (uint32_t*)c->enc_send.p, c->codec_scr.p, scr, d_sz, s)
+                          : misort::codec_encode_dev<uint64_t>((const uint64_t*)base, run, kmax,
+                                                               (uint32_t*)c->enc_send.p, c->codec_scr.p, scr, d_sz, s);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "codec_encode: %s", hipGetErrorString(e));
     // every side sends whichever of coded and raw is smaller; the receiver tells
-    // them apart by the size (coded < raw).  The coded word count stays on the
-    // device: the ranks exchange (coded, raw) word counts straight from device
-    // memory, then one host sync serves both the choice and the sizes.
-    int64_t* d_sz = (int64_t*)c->small.p + 2;  // [coded words, raw words]
-    HIPCHK(hipMemsetAsync(d_sz, 0, 16, s));
-    HIPCHK(hipMemcpyAsync(d_sz, d_total, 4, hipMemcpyDeviceToDevice, s));  // low word (little-endian)
-    HIPCHK(hipMemcpyAsync(d_sz + 1, &raw_words, 8, hipMemcpyHostToDevice, s));
+    // them apart by the size (coded < raw)
     std::vector<int64_t> all, m;
     const int me = c->rank;
     if (relayed) {
@@ -661,9 +660,19 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sb
         HIPCHK(hipMemcpyAsync(&all[(size_t)2 * q], d_sz + 2, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    const int64_t raw_words = all[(size_t)2 * me + 1];
+    const int64_t k = raw_words * 4 / (int64_t)w;
+    // both partners derive k from the same samples
+    if (all[(size_t)2 * q + 1] != raw_words || k < 0 || k > kmax)
+        return fail(MISORT_E_INVALID, "exchange count mismatch (%lld vs %lld words)", (long long)raw_words,
+                    (long long)all[(size_t)2 * q + 1]);
+    *k_out = k;
     auto units = [&](int r) { return std::min(all[(size_t)2 * r], all[(size_t)2 * r + 1]); };  // 4-byte words sent
     const bool use = all[(size_t)2 * me] < raw_words;
-    const void* msg = use ? c->enc_send.p : sbuf;
+    // the raw message is the run itself: the keep-max side's bottom k keys, the
+    // keep-min side's top k (run[0] on the device)
+    const int64_t off = keep_max ? 0 : nloc - k;
+    const void* msg = use ? c->enc_send.p : (const char*)base + (size_t)off * w;
     const size_t mbytes = (size_t)units(me) * 4;
     if (mbytes != (use ? (size_t)all[(size_t)2 * me] * 4 : (size_t)k * w))
         return fail(MISORT_E_INVALID, "coded message size");
@@ -673,10 +682,11 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* sb
         size_t rb2 = 0;
         rc = relay_exchange(c, 4, ilog2(q ^ c->rank), msg, mbytes, c->enc_recv.p, c->enc_recv.bytes, s, &rb2, &m);
         if (!rc && rb2 != rb) return fail(MISORT_E_INVALID, "relay: partner size mismatch");
-    } else {
+    } else if (k > 0) {
         rc = c->tr->sendrecv(msg, mbytes, c->enc_recv.p, rb, q, s);
     }
     if (rc) return rc;
+    if (k == 0) return MISORT_OK;
     c->xchg_bytes += (int64_t)(mbytes + rb);
     c->xchg_raw_bytes += (int64_t)(2 * k * w);
     if ((int64_t)rb >= raw_words * 4) {  // sent uncoded
@@ -740,12 +750,27 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     void* cur = (nst & 1) ? work : out;
     misort::StageIO lio;
     const bool chunk_out = io && io->after_last && nst == 0;
+    bool chunked = false;  // the local sort's last pass handed its output over chunk by chunk
     if (io) {
         lio = *io;
-        if (!chunk_out) lio.after_last = nullptr;
+        if (!chunk_out) {
+            lio.after_last = nullptr;
+        } else {
+            const auto after = io->after_last;
+            lio.after_last = [&chunked, after](int64_t k0, int64_t k1, hipStream_t st) {
+                chunked = true;
+                return after(k0, k1, st);
+            };
+        }
     }
     if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s, io ? &lio : nullptr))) return rc;
-    if (chunk_out) return MISORT_OK;
+    if (chunk_out && chunked) return MISORT_OK;  // after_last owned the f64 back-conversion
+    if (chunk_out) {
+        // a last pass that is not chunked (a multi-way pass): the caller copies
+        // the whole block out, converted here
+        if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)cur, loc, s));
+        return MISORT_OK;
+    }
     void* other = (cur == work) ? out : work;
     misort::LaunchHook* hk = hook(c);
     struct StageMark {  // attributes profiled launches to the hypercube stage
@@ -770,9 +795,17 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         // min side = "A" (keeps its n_a smallest), max side = "B"
         const int64_t na = mx ? nq : loc, nb = mx ? loc : nq;
         int64_t k;  // keys each side sends: A's top k, B's bottom k
-        if (c->full_exchange || loc == 0 || nq == 0) {
-            k = -1;
-        } else {
+        const bool relayed = c->relay && p > 2;
+        const void* rkeys = c->recv.p;
+        const int64_t moved0 = c->xchg_bytes;
+        if ((rc = c->small.ensure(64))) return rc;
+        int64_t* d_run = (int64_t*)c->small.p + 4;  // {send offset, k} on the device
+        // the codec's offsets and word totals are 32-bit: messages that could
+        // reach 2^32 words go raw (both sides decide from the same bound)
+        const int64_t kmax = std::min(na, nb);
+        const bool coded = !c->full_exchange && loc > 0 && nq > 0 && c->compress &&
+                           misort::codec_max_words(kmax, (int)w) < ((int64_t)1 << 32);
+        if (!c->full_exchange && loc > 0 && nq > 0) {
             const int64_t cm = sample_count(loc), cq = sample_count(nq);
             hipError_t e = w == 4 ? misort::gather_samples<uint32_t>((const uint32_t*)cur, loc, sample_stride(loc),
                                                                      (uint32_t*)c->samp_me.p, cm, s)
@@ -781,6 +814,33 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             if (e != hipSuccess) return fail(MISORT_E_HIP, "gather_samples: %s", hipGetErrorString(e));
             if ((rc = c->tr->sendrecv(c->samp_me.p, (size_t)cm * w, c->samp_peer.p, (size_t)cq * w, q, s)))
                 return rc;
+        }
+        c->xchg_stages += 1;
+        c->xchg_full_bytes += (int64_t)((loc + nq) * w);
+        if (coded) {
+            // k on the device; the host learns it in the stage's one size exchange
+            const void* sa = mx ? c->samp_peer.p : c->samp_me.p;
+            const void* sb = mx ? c->samp_me.p : c->samp_peer.p;
+            hipError_t e = w == 4 ? misort::exchange_count<uint32_t>((const uint32_t*)sa, na, (const uint32_t*)sb,
+                                                                     nb, mx, loc, d_run, s)
+                                  : misort::exchange_count<uint64_t>((const uint64_t*)sa, na, (const uint64_t*)sb,
+                                                                     nb, mx, loc, d_run, s);
+            if (e != hipSuccess) return fail(MISORT_E_HIP, "exchange_count: %s", hipGetErrorString(e));
+            if ((rc = coded_exchange(c, dtype, q, relayed, cur, loc, mx, d_run, kmax, &k, &rkeys, s))) return rc;
+            if (k == 0) {  // no key crosses: both blocks stay as they are
+                xg_close(0.0);
+                continue;
+            }
+            xg_close((double)(c->xchg_bytes - moved0));
+            if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, k, other, keep[st], s))) return rc;
+            std::swap(cur, other);
+            continue;
+        }
+        if (c->full_exchange || loc == 0 || nq == 0) {
+            k = -1;
+        } else {
+            // raw exchange: k from the samples on the host
+            const int64_t cm = sample_count(loc), cq = sample_count(nq);
             int64_t ilo;
             if (w == 4) {
                 std::vector<uint32_t> me(cm), pe(cq);
@@ -797,9 +857,6 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             }
             k = na - ilo;
         }
-        c->xchg_stages += 1;
-        c->xchg_full_bytes += (int64_t)((loc + nq) * w);
-        const bool relayed = c->relay && p > 2;
         if (k == 0) {  // no key crosses: both blocks stay as they are
             // relay units are 4 bytes on every rank of the stage (coded messages are words)
             if (relayed && (rc = relay_raw(c, ilog2(q ^ c->rank), cur, 0, c->recv.p, 0, s))) return rc;
@@ -820,21 +877,11 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             sbytes = rbytes = (size_t)k * w;
             nrecv = k;
         }
-        const void* rkeys = c->recv.p;
-        const int64_t moved0 = c->xchg_bytes;
-        // the codec's offsets and word totals are 32-bit: messages that could
-        // reach 2^32 words go raw (both sides decide from k alone)
-        if (k > 0 && c->compress && misort::codec_max_words(k, (int)w) < ((int64_t)1 << 32)) {
-            // delta-code the sorted run; each side sends whichever of coded and raw is
-            // smaller, and the receiver tells them apart by size (coded < raw)
-            if ((rc = coded_exchange(c, dtype, q, relayed, sbuf, k, &rkeys, s))) return rc;
-        } else {
-            if (relayed) rc = relay_raw(c, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
-            else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
-            if (rc) return rc;
-            c->xchg_bytes += (int64_t)(sbytes + rbytes);
-            c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
-        }
+        if (relayed) rc = relay_raw(c, ilog2(q ^ c->rank), sbuf, sbytes, c->recv.p, rbytes, s);
+        else rc = c->tr->sendrecv(sbuf, sbytes, c->recv.p, rbytes, q, s);
+        if (rc) return rc;
+        c->xchg_bytes += (int64_t)(sbytes + rbytes);
+        c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
         xg_close((double)(c->xchg_bytes - moved0));
         if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
         std::swap(cur, other);
@@ -1272,9 +1319,9 @@ int misort_codec_probe(misort_ctx* c, int dtype, const void* keys, int64_t n, in
     hipError_t e = hipSuccess;
     auto enc = [&] {
         return w == 4 ? misort::codec_encode<uint32_t>((const uint32_t*)keys, n, (uint32_t*)c->enc_send.p,
-                                                      c->codec_scr.p, scr, (uint32_t*)c->small.p, s)
+                                                      c->codec_scr.p, scr, (int64_t*)c->small.p, s)
                       : misort::codec_encode<uint64_t>((const uint64_t*)keys, n, (uint32_t*)c->enc_send.p,
-                                                      c->codec_scr.p, scr, (uint32_t*)c->small.p, s);
+                                                      c->codec_scr.p, scr, (int64_t*)c->small.p, s);
     };
     auto dec = [&] {
         return w == 4 ? misort::codec_decode<uint32_t>((const uint32_t*)c->enc_send.p, n, (uint32_t*)out, s)
@@ -1287,8 +1334,8 @@ int misort_codec_probe(misort_ctx* c, int dtype, const void* keys, int64_t n, in
     for (int i = 0; i < reps && e == hipSuccess; ++i) e = dec();
     if (e == hipSuccess) e = hipEventRecord(e2, s);
     if (e == hipSuccess) e = hipEventSynchronize(e2);
-    uint32_t words = 0;
-    if (e == hipSuccess) e = hipMemcpy(&words, c->small.p, 4, hipMemcpyDeviceToHost);
+    int64_t words = 0;
+    if (e == hipSuccess) e = hipMemcpy(&words, c->small.p, 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && enc_ms) e = hipEventElapsedTime(enc_ms, e0, e1);
     if (e == hipSuccess && dec_ms) e = hipEventElapsedTime(dec_ms, e1, e2);
     (void)hipEventDestroy(e0);
@@ -1297,7 +1344,7 @@ int misort_codec_probe(misort_ctx* c, int dtype, const void* keys, int64_t n, in
     HIPCHK(e);
     if (enc_ms) *enc_ms /= reps;
     if (dec_ms) *dec_ms /= reps;
-    if (coded_bytes) *coded_bytes = (int64_t)words * 4;
+    if (coded_bytes) *coded_bytes = words * 4;
     return MISORT_OK;
 }
 
