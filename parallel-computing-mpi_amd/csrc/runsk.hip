@@ -100,7 +100,7 @@ struct Shape {
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_KEYS = PAD + CAP + K * (G + IT) + 16;
-    static_assert(FM > 0, "fence stride too coarse for the chunk");
+    static_assert(FM > 0 && FM < 256, "fence stride vs chunk (k_fence_counts keeps 8-bit counts)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
     static_assert(CAP + (K / 2) * (G + IT) <= NT * IT, "level layout: pairs at lane boundaries");
     static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS key index of a row fits 16 bits");
@@ -259,7 +259,8 @@ __global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const FT* __restrict__
     __shared__ int sw[SCAN_NT / 64];
     const int64_t c = (int64_t)blockIdx.x * SCAN_NT + threadIdx.x;
     const int K = geo.K();
-    int cnt[16] = {};
+    // per-run counts (<= FM < 256) as 8-bit fields: runs 0..7 in lo, 8..15 in hi
+    uint64_t lo8 = 0, hi8 = 0;
     if (c < nchunks) {
         int64_t g, t;
         chunk_place(geo, c, g, t);
@@ -268,13 +269,15 @@ __global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const FT* __restrict__
         const int64_t e1 = e0 + geo.fm < nf ? e0 + geo.fm : nf;
         for (int64_t e = e0; e < e1; ++e) {
             const int r = (int)((ftag(m[e]) >> (32 - geo.lk)) & (K - 1));
-#pragma unroll
-            for (int q = 0; q < 16; ++q) cnt[q] += q == r;
+            const uint64_t one = 1ull << (8 * (r & 7));
+            if (r < 8) lo8 += one;
+            else hi8 += one;
         }
     }
     for (int q = 0; q < K; ++q) {
-        const int inc = block_scan(cnt[q], sw);
-        if (c < nchunks) P[c * K + q] = inc - cnt[q];
+        const int cq = (int)(((q < 8 ? lo8 : hi8) >> (8 * (q & 7))) & 0xFF);
+        const int inc = block_scan(cq, sw);
+        if (c < nchunks) P[c * K + q] = inc - cq;
         if (threadIdx.x == SCAN_NT - 1) bsum[(int64_t)blockIdx.x * K + q] = inc;
     }
 }
