@@ -74,10 +74,12 @@ struct PlanKnobs {
     // (0 = network only), per key type.  Measured at 2^30 u32 / 2^29 u64: the
     // SORT tile's level is best (profiles/r01/runs/).
     int merge_from_u32 = 15, merge_from_u64 = 13;
-    // u32 sorts of at most 2^merge_min_log2 keys (cache-resident: 2^24 u32 is
-    // 64 MiB) stay on the network, whose passes are shorter there (2^24:
-    // 0.60 vs 0.63 ms, 2^20: 0.18 vs 0.21 ms; 2^28: 10.3 vs 6.8 ms).
-    int merge_min_log2_u32 = 24;
+    // u32 sorts of at most 2^merge_min_log2 keys (cache-resident) stay on the
+    // network, whose passes are shorter there.  Against the multi-way passes
+    // (round 2, profiles/r02/s2f): 2^20 0.171 vs 0.183 ms, 2^22 0.255 vs
+    // 0.296, but 2^24 0.580 vs 0.479 ms (three 8-way passes beat ~14 network
+    // passes), so 2^24 (BASELINE config 2) now takes the merge passes.
+    int merge_min_log2_u32 = 23;
     // u32 merge levels: up to this many levels per multi-way pass (runsk.hip,
     // 2^lk-way, lk <= 4); 0 or 1: one 2-way pass per level (MISORT_MULTIWAY).
     // 3 measured best at 2^30: 63.8 Gkeys/s vs 62.6 with 16-way passes (a 4th

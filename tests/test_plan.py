@@ -135,7 +135,8 @@ def test_plan_pass_counts():
     assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [3, 3, 3, 3, 2]
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
-    assert len(misort.plan(1 << 24, 4)) == 15  # cache-resident u32 sizes stay on the network
+    assert len(misort.plan(1 << 23, 4)) == 13  # cache-resident u32 sizes stay on the network
+    assert [q[0] for q in misort.plan(1 << 24, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^24: 3 x 8-way
     # u64: 2^13-key SORT tiles, then 16 levels in six multi-way passes
     # (128-bit fences; 2-way passes would be 1 + 16)
     p29 = misort.plan((1 << 29) - 3, 8)
@@ -223,7 +224,7 @@ def test_plans_merge_from(mfrom):
         if mfrom == "0":
             assert m0 == k
         else:
-            assert m0 == (int(mfrom) if int(mfrom) < k and k > 24 else k)  # MISORT_MERGE_MIN_LOG2 = 24
+            assert m0 == (int(mfrom) if int(mfrom) < k and k > 23 else k)  # MISORT_MERGE_MIN_LOG2 = 23
         assert plan_stages(p, lt) == network(min(k, m0), lt)
         if n <= 1 << 18:
             rng = np.random.default_rng(n)
