@@ -58,7 +58,9 @@ enum misort_kernel_kind {
     MISORT_K_RUN_MERGE = 7,   /* one merge level: runs 2^hi -> 2^(hi+1)  */
     MISORT_K_EXCHANGE = 8,    /* compare-split exchange leg (splitter samples, RCCL
                                  send/recv, codec), device time between events */
-    MISORT_K_RUN_MERGE4 = 9   /* two merge levels in one pass: runs 2^hi -> 2^(hi+2) */
+    MISORT_K_RUN_MERGE4 = 9,  /* a multi-way pass: lk merge levels, runs 2^hi -> 2^(hi+lk) */
+    MISORT_K_RUN_MERGEK_KERNEL = 10 /* the merge kernel of a multi-way pass alone (its planning
+                                       kernels excluded; nested in MISORT_K_RUN_MERGE4) */
 };
 
 typedef struct misort_ctx misort_ctx;

@@ -1480,7 +1480,7 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
         if (p.kind == KIND_RUNSK) {
             const bool prevk = i > 0 && (ps[i - 1].kind == KIND_RUNSK || (i == 1 && sort_fences));
             const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
-            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next);
+            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, hook);
             if (e != hipSuccess) return e;
             fence_phase ^= 1;
             src = dst;

@@ -20,7 +20,8 @@ enum Kind : int {
     KIND_RUNS = 7,        // one merge level: runs of 2^hi keys -> runs of 2^(hi+1)
     KIND_EXCHANGE = 8,    // compare-split exchange leg (samples, RCCL send/recv, codec); not a kernel
     KIND_RUNSK = 9,       // R merge levels in one pass: runs of 2^hi -> 2^(hi+R), 2^R-way (runsk.hip)
-    KIND_COUNT = 10
+    KIND_RUNSK_KERNEL = 10,  // the k_mergek launch of a KIND_RUNSK pass alone (nested in it)
+    KIND_COUNT = 11
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with
@@ -92,11 +93,11 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
 // into the other buffer.  15 <= lw, lw + lk <= 30; src != dst; buffers 16-byte
 // aligned.
 hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next);
+                        bool gather, int lk_next, LaunchHook* hook = nullptr);
 // u64 keys: the same with 128-bit fences (key << 64 | run/position tag);
 // 13 <= lw, lw + lk <= 29.
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next);
+                        bool gather, int lk_next, LaunchHook* hook = nullptr);
 int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
 // Fence stride of the multi-way passes (log2 keys).
 #ifndef MISORT_MK_FG_LOG2

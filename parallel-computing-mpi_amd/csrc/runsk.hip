@@ -788,7 +788,7 @@ int64_t chunks_of(const Geo& geo) {
 
 template <typename KEY, int LK>
 hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
-                      int lk_next) {
+                      int lk_next, LaunchHook* hook) {
     typedef Shape<KEY, LK> S;
     typedef typename KTr<KEY>::F FT;
     const Geo geo = make_geo<KEY>(n, lw, LK);
@@ -849,8 +849,10 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         <<<(unsigned)((nchunks + DESC_CPB * DESC_CPW - 1) / (DESC_CPB * DESC_CPW)), 64 * DESC_CPB, 0, s>>>(
             bounds, geo, nchunks, desc);
     const unsigned grid = (unsigned)nchunks;
+    if (hook) hook->before(KIND_RUNSK_KERNEL, 2.0 * (double)n * sizeof(KEY), s);
     if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
     else k_mergek<KEY, LK, false><<<grid, S::NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
+    if (hook) hook->after(KIND_RUNSK_KERNEL, s);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
     if (probe) {
         // same chunks, outputs to a scratch buffer (the sort is untouched)
@@ -870,17 +872,17 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
 
 template <typename KEY>
 hipError_t merge_levelk_t(const KEY* src, KEY* dst, int64_t n, int lw, int lk, hipStream_t s, int phase, bool gather,
-                          int lk_next) {
+                          int lk_next, LaunchHook* hook) {
     if (n <= 0) return hipSuccess;
     // load rows address a group with 32-bit byte offsets (KW * sizeof(KEY) <=
     // 2^32); runs at least a SORT tile long
     if (lk < 1 || lk > 4 || lw < KTr<KEY>::LW_MIN || lw + lk > KTr<KEY>::LWK_MAX || src == dst || lk_next < 0 ||
         lk_next > 4)
         return hipErrorInvalidValue;
-    if (lk == 1) return merge_pass<KEY, 1>(src, dst, n, lw, s, phase, gather, lk_next);
-    if (lk == 2) return merge_pass<KEY, 2>(src, dst, n, lw, s, phase, gather, lk_next);
-    if (lk == 3) return merge_pass<KEY, 3>(src, dst, n, lw, s, phase, gather, lk_next);
-    return merge_pass<KEY, 4>(src, dst, n, lw, s, phase, gather, lk_next);
+    if (lk == 1) return merge_pass<KEY, 1>(src, dst, n, lw, s, phase, gather, lk_next, hook);
+    if (lk == 2) return merge_pass<KEY, 2>(src, dst, n, lw, s, phase, gather, lk_next, hook);
+    if (lk == 3) return merge_pass<KEY, 3>(src, dst, n, lw, s, phase, gather, lk_next, hook);
+    return merge_pass<KEY, 4>(src, dst, n, lw, s, phase, gather, lk_next, hook);
 }
 
 }  // namespace
@@ -894,12 +896,12 @@ int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes) {
 // pass's fences (runs of 2^(lw+lk) in groups of 2^lk_next) into the other
 // buffer.
 hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next) {
-    return merge_levelk_t<uint32_t>(src, dst, n, lw, lk, s, phase, gather, lk_next);
+                        bool gather, int lk_next, LaunchHook* hook) {
+    return merge_levelk_t<uint32_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook);
 }
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next) {
-    return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next);
+                        bool gather, int lk_next, LaunchHook* hook) {
+    return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook);
 }
 void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
     // the sizes merge_pass computes, so the buffer never moves between the two

@@ -80,7 +80,8 @@ struct Profiler final : misort::LaunchHook {
     double st_ms[MAX_STAGES][2] = {};
     double st_bytes[MAX_STAGES] = {};
     int stage = -1;
-    Rec cur{};
+    Rec cur{};               // the innermost open record (the exchange leg sets its bytes)
+    std::vector<Rec> open;   // enclosing records (a pass around its kernel)
     bool on = false;
 
     hipEvent_t take() {
@@ -94,12 +95,19 @@ struct Profiler final : misort::LaunchHook {
         return e;
     }
     void before(misort::Kind k, double b, hipStream_t s) override {
+        if (cur.kind >= 0 && (cur.a || cur.b)) open.push_back(cur);
         cur = Rec{k, take(), take(), b, stage};
         if (cur.a) (void)hipEventRecord(cur.a, s);
     }
     void after(misort::Kind, hipStream_t s) override {
         if (cur.b) (void)hipEventRecord(cur.b, s);
         pending.push_back(cur);
+        if (!open.empty()) {
+            cur = open.back();
+            open.pop_back();
+        } else {
+            cur = Rec{-1, nullptr, nullptr, 0.0, -1};
+        }
     }
     int collect() {
         for (auto& r : pending) {

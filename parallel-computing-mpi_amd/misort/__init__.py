@@ -24,7 +24,7 @@ __all__ = [
 
 U32, U64, F64 = 0, 1, 2
 KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other", "span_pass",
-              "wide_pass", "run_merge", "exchange", "run_mergek"]
+              "wide_pass", "run_merge", "exchange", "run_mergek", "run_mergek_kernel"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.environ.get("MISORT_LIBRARY") or os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
