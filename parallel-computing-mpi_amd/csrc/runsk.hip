@@ -90,6 +90,8 @@ constexpr KEY KMAX = (KEY)~(KEY)0;
 // boundaries past the previous pair's sentinels (no lane straddles two pairs).
 constexpr int PAD = 4;  // keys below the tile: a co-rank probe may read index -1
 
+constexpr int SCAN_NT_MAX = 256;  // chunks per fence-count block (SCAN_NT below)
+
 template <typename KEY, int LK>
 struct Shape {
     typedef KTr<KEY> T;
@@ -100,7 +102,8 @@ struct Shape {
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_KEYS = PAD + CAP + K * (G + IT) + 16;
-    static_assert(FM > 0 && FM < 256, "fence stride vs chunk (k_fence_counts keeps 8-bit counts)");
+    static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
+                  "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
     static_assert(CAP + (K / 2) * (G + IT) <= NT * IT, "level layout: pairs at lane boundaries");
     static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS key index of a row fits 16 bits");
@@ -230,15 +233,16 @@ __device__ __forceinline__ void chunk_place(const Geo& geo, int64_t c, int64_t& 
     }
 }
 
-constexpr int SCAN_NT = 256;  // chunks per block of the fence-count scan
+constexpr int SCAN_NT = SCAN_NT_MAX;  // chunks per block of the fence-count scan
 
-// Inclusive scan of v over the block (SCAN_NT lanes, 4 waves of 64).
-__device__ __forceinline__ int block_scan(int v, int* sw) {
+// Inclusive scan of a u64 over the block (all its lanes; sw holds one entry
+// per wave), for packed fields.
+__device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(v, o, 64);
-        v += lane >= o ? u : 0;
+        const uint64_t u = __shfl_up(v, o, 64);
+        v += lane >= o ? u : 0ull;
     }
     if (lane == 63) sw[w] = v;
     __syncthreads();
@@ -252,47 +256,79 @@ __device__ __forceinline__ int block_scan(int v, int* sw) {
 // chunks, P = the scan within the block, bsum = the block totals.  A run's
 // fences before a chunk-start fence = P(c) - P(group's first chunk), with the
 // block totals scanned in (k_scan_totals) -- this replaces a binary search of
-// each run's fence list.
+// each run's fence list.  The block's chunks own one contiguous range of M;
+// its lanes read that range coalesced and add each fence to its chunk's
+// counters in LDS (8-bit fields, runs 0..7 and 8..15 in two u64 words;
+// one lane per chunk reading its own FM fences ran 49 us at 2^30).
+// lanes of a fence-count block (SCAN_NT chunks): 1024 measured slower (46.8
+// vs 41.5 us at 2^30: the lanes of a wave add to the same few chunk counters)
+constexpr int COUNT_NT = SCAN_NT;
 template <typename FT>
-__global__ __launch_bounds__(SCAN_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
-                                                          int* __restrict__ P, int* __restrict__ bsum) {
-    __shared__ int sw[SCAN_NT / 64];
-    const int64_t c = (int64_t)blockIdx.x * SCAN_NT + threadIdx.x;
+__global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
+                                                           int* __restrict__ P, int* __restrict__ bsum) {
+    __shared__ uint64_t sws[COUNT_NT / 64];
+    __shared__ unsigned long long sc[SCAN_NT][2];
+    const int tid = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * SCAN_NT, c = c0 + tid;
+    const int64_t c1 = c0 + SCAN_NT < nchunks ? c0 + SCAN_NT : nchunks;
     const int K = geo.K();
-    // per-run counts (<= FM < 256) as 8-bit fields: runs 0..7 in lo, 8..15 in hi
-    uint64_t lo8 = 0, hi8 = 0;
-    if (c < nchunks) {
-        int64_t g, t;
-        chunk_place(geo, c, g, t);
-        const FT* m = M + (geo.base(g) >> FG_LOG2);
-        const int64_t e0 = t * geo.fm, nf = geo.nfences(g);
-        const int64_t e1 = e0 + geo.fm < nf ? e0 + geo.fm : nf;
-        for (int64_t e = e0; e < e1; ++e) {
-            const int r = (int)((ftag(m[e]) >> (32 - geo.lk)) & (K - 1));
-            const uint64_t one = 1ull << (8 * (r & 7));
-            if (r < 8) lo8 += one;
-            else hi8 += one;
-        }
+    const int gl = geo.lw + geo.lk;
+    if (tid < SCAN_NT) sc[tid][0] = sc[tid][1] = 0ull;
+    __syncthreads();
+    int64_t g, t;
+    chunk_place(geo, c0, g, t);
+    const int64_t f0 = (geo.base(g) >> FG_LOG2) + t * geo.fm;
+    chunk_place(geo, c1 - 1, g, t);
+    const int64_t gf = geo.base(g) >> FG_LOG2, nfg = geo.nfences(g);
+    const int64_t f1 = t * geo.fm + geo.fm < nfg ? gf + t * geo.fm + geo.fm : gf + nfg;
+    for (int64_t e = f0 + tid; e < f1; e += COUNT_NT) {
+        int64_t ge = (e << FG_LOG2) >> gl;  // the fence's group (the tail group starts at nfull)
+        ge = ge < geo.nfull ? ge : geo.nfull;
+        const int64_t ce = ge * geo.kf + (e - (geo.base(ge) >> FG_LOG2)) / geo.fm;
+        const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
+        atomicAdd(&sc[ce - c0][r >> 3], 1ull << (8 * (r & 7)));
     }
-    for (int q = 0; q < K; ++q) {
-        const int cq = (int)(((q < 8 ? lo8 : hi8) >> (8 * (q & 7))) & 0xFF);
-        const int inc = block_scan(cq, sw);
-        if (c < nchunks) P[c * K + q] = inc - cq;
-        if (threadIdx.x == SCAN_NT - 1) bsum[(int64_t)blockIdx.x * K + q] = inc;
+    __syncthreads();
+    // scan 4 runs at a time as 16-bit fields of one u64 (block prefixes <=
+    // SCAN_NT * FM < 2^16): K/4 block scans instead of K
+    const uint64_t w8[2] = {tid < SCAN_NT ? sc[tid][0] : 0ull, tid < SCAN_NT ? sc[tid][1] : 0ull};
+    for (int q0 = 0; q0 < K; q0 += 4) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = q0 + j;
+            v |= ((w8[q >> 3] >> (8 * (q & 7))) & 0xFFull) << (16 * j);
+        }
+        const uint64_t inc = block_scan_u64(v, sws);
+        const int nq = K - q0 < 4 ? K - q0 : 4;
+        for (int j = 0; j < nq; ++j) {
+            const int q = q0 + j;
+            const int vi = (int)((inc >> (16 * j)) & 0xFFFF), vq = (int)((v >> (16 * j)) & 0xFFFF);
+            if (tid < SCAN_NT && c < nchunks) P[c * K + q] = vi - vq;
+            if (threadIdx.x == SCAN_NT - 1) bsum[(int64_t)blockIdx.x * K + q] = vi;
+        }
     }
 }
 
-// Exclusive scan of the block totals (one workgroup, carried over rounds).
+// Exclusive scan of the block totals (one workgroup, carried over rounds),
+// two runs at a time as 32-bit fields of one u64 (totals < 2^31).
 __global__ __launch_bounds__(SCAN_NT) void k_scan_totals(int* __restrict__ bsum, int64_t nb, int K) {
-    __shared__ int sw[SCAN_NT / 64];
-    __shared__ int tot;
-    for (int q = 0; q < K; ++q) {
-        int carry = 0;
+    __shared__ uint64_t sw[SCAN_NT / 64];
+    __shared__ uint64_t tot;
+    for (int q = 0; q < K; q += 2) {
+        const bool two = q + 1 < K;
+        uint64_t carry = 0;
         for (int64_t b0 = 0; b0 < nb; b0 += SCAN_NT) {
             const int64_t b = b0 + threadIdx.x;
-            const int v = b < nb ? bsum[b * K + q] : 0;
-            const int inc = block_scan(v, sw);
-            if (b < nb) bsum[b * K + q] = carry + inc - v;
+            const uint64_t v = b < nb ? (uint64_t)(uint32_t)bsum[b * K + q] |
+                                            (two ? (uint64_t)(uint32_t)bsum[b * K + q + 1] << 32 : 0ull)
+                                      : 0ull;
+            const uint64_t inc = block_scan_u64(v, sw);
+            const uint64_t ex = carry + inc - v;
+            if (b < nb) {
+                bsum[b * K + q] = (int)(uint32_t)ex;
+                if (two) bsum[b * K + q + 1] = (int)(uint32_t)(ex >> 32);
+            }
             if (threadIdx.x == SCAN_NT - 1) tot = inc;
             __syncthreads();
             carry += tot;
@@ -841,7 +877,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         }
     }
     const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
-    k_fence_counts<FT><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    k_fence_counts<FT><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
     k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots,
                                                                           bounds);
