@@ -58,13 +58,21 @@ typedef unsigned __int128 u128;
 // merged in LDS (64 KiB).
 template <typename KEY>
 struct KTr;
+// Build-time probes (tools/build_variant.sh): the u32 chunk capacity and the
+// workgroups per CU its LDS tile allows.
+#ifndef MISORT_MK_CAP
+#define MISORT_MK_CAP 0
+#endif
+#ifndef MISORT_MK_WGCU
+#define MISORT_MK_WGCU 0
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
     static constexpr int NT = MISORT_MK_NT;
     static constexpr int IT = NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
-    static constexpr int CAP = NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
-    static constexpr int WG_PER_CU = NT == 1024 ? 2 : 4;    // ~34 KiB tiles; 8 waves per SIMD at NT = 512
+    static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
+    static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = 15, LWK_MAX = 30;         // runs >= the SORT tile; 32-bit row offsets
 };
@@ -585,7 +593,10 @@ __global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __r
 // and [B0, B0 + LB].
 template <typename KEY>
 __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
-    constexpr int CO_STEP0 = KTr<KEY>::CAP / 2;  // first co-rank step: hi - lo <= CAP/2
+    // first co-rank step: the largest power of two <= CAP/2 (hi - lo <= CAP/2;
+    // the steps must be powers of two for the lifting search)
+    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(KTr<KEY>::CAP / 2)));
+    static_assert(KTr<KEY>::CAP / 2 <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
     const KEY* a = s + A0 - 1;
