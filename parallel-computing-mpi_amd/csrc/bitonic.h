@@ -693,13 +693,14 @@ __host__ __device__ constexpr bool pgroup_rep(int k, int cnt, int top, bool flip
 // LDS -> registers (final slot window SF, mirrored upper slots if MF) -> the
 // pass's last register stages -> HBM.  Slots are handled one stage-connected
 // group at a time, so only 2^CNT vectors are live.
-// fence (SORT tiles of u32 keys only, may be null): the first multi-way merge
-// pass's fences, written here instead of gathered from HBM by k_fence_gather
-// -- the key at every 2^MERGEK_FENCE_LOG2-th position of the sorted tile,
-// packed as runsk.hip's fpack does for runs of 2^LT keys in groups of 2^flk.
+// fence (SORT tiles only, may be null): the first multi-way merge pass's
+// fences, written here instead of gathered from HBM by k_fence_gather -- the
+// key at every 2^MERGEK_FENCE_LOG2-th position of the sorted tile, packed as
+// runsk.hip's fpack does for runs of 2^LT keys in groups of 2^flk (u32 keys:
+// 64-bit fences, u64 keys: 128-bit).
 template <typename K, int LT, int MODE, int SF, bool MF, int TOP, int CNT, bool FLIP, bool COMP>
 __device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m, int64_t tile, int64_t n,
-                                            bool full, int t, uint64_t* fence = nullptr, int flk = 0) {
+                                            bool full, int t, void* fence = nullptr, int flk = 0) {
     typedef TileGeo<K, LT> G;
     constexpr int NG = 1 << CNT;
 #pragma unroll
@@ -743,14 +744,18 @@ __device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m
             for (int j = 0; j < G::V; ++j) x[j] = mk ? w[S][G::V - 1 - j] : w[S][j];
             const int e = place<K, LT, SF>(k, slot_lane<K, LT, MF>(k, t));
             store_slot<K, LT, MODE>(out, m, tile, n, full, e, x);
-            if constexpr (MODE == TM_SORT && sizeof(K) == 4) {
+            if constexpr (MODE == TM_SORT) {
                 constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
                 const int64_t gi = (tile << LT) + e;
-                if (fence && (e & FGM) == 0 && gi < n)
-                    fence[gi >> MERGEK_FENCE_LOG2] =
-                        ((uint64_t)x[0] << 32) |
-                        ((uint64_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
-                        (uint64_t)((e & ((1 << LT) - 1)) >> MERGEK_FENCE_LOG2);
+                if (fence && (e & FGM) == 0 && gi < n) {
+                    const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
+                                         (uint32_t)((e & ((1 << LT) - 1)) >> MERGEK_FENCE_LOG2);
+                    if constexpr (sizeof(K) == 4)
+                        ((uint64_t*)fence)[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
+                    else
+                        ((unsigned __int128*)fence)[gi >> MERGEK_FENCE_LOG2] =
+                            ((unsigned __int128)x[0] << 64) | tag;
+                }
             }
         }
     }
@@ -761,7 +766,7 @@ __device__ __forceinline__ void final_store(const K* s, K* out, const TileMap& m
 // (no prefetch registers live across the LDS phases).
 template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD, bool PERSIST>
 __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_stream(
-    const K* in, K* out, int64_t n, TileMap m) {
+    const K* in, K* out, int64_t n, TileMap m, void* fence, int flk) {
     typedef TileGeo<K, LT> G;
     constexpr ProgPlan P = prog_plan(ProgGeo{LT, G::KB, G::VB, MODE, R, FLIP, PERSIST ? 2 : G::KB});
     constexpr int SL = MODE == TM_SORT ? LT - G::KB : P.SL;
@@ -848,7 +853,7 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
             // LDS -> registers (final slot window) -> last stages -> HBM
             constexpr int SF = MODE == TM_SORT ? LT - G::KB : P.SF;
             final_store<K, LT, MODE, SF, P.MFIN, P.POST_TOP, P.POST, P.POST_FLIP, P.COMP>(s, out, m, tile, n,
-                                                                                        full, t);
+                                                                                        full, t, fence, flk);
             __syncthreads();
         }
         if constexpr (!PERSIST) break;
@@ -875,8 +880,10 @@ struct HookScope {
 };
 
 
+// fence/flk: SORT passes only, see final_store (null: no fences).
 template <typename K, int LT, int MODE, int R, bool FLIP, bool ORD>
-void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s) {
+void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t s, void* fence = nullptr,
+                   int flk = 0) {
     typedef TileGeo<K, LT> G;
     static int64_t cap = 0;  // resident workgroups for this instantiation
     const bool persist = (plan_knobs().persist_mask((int)sizeof(K)) >> MODE) & 1;
@@ -891,8 +898,8 @@ void launch_stream(const K* in, K* out, int64_t n, const TileMap& m, hipStream_t
     const int64_t want = persist ? cap * plan_knobs().grid_mult : m.ntiles;
     const int64_t grid = m.ntiles < want ? m.ntiles : want;
     if (grid <= 0) return;
-    if (persist) k_stream<K, LT, MODE, R, FLIP, ORD, true><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
-    else k_stream<K, LT, MODE, R, FLIP, ORD, false><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m);
+    if (persist) k_stream<K, LT, MODE, R, FLIP, ORD, true><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m, fence, flk);
+    else k_stream<K, LT, MODE, R, FLIP, ORD, false><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, m, fence, flk);
 }
 
 template <typename K, int LT, int MODE, int R>
@@ -1434,15 +1441,15 @@ inline bool sort_u32_path() { return MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 1
 // One pass of a plan over n keys, src -> dst.
 template <typename K, int LT, int LTR>
 void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hipStream_t s,
-                 uint64_t* fence = nullptr, int flk = 0) {
+                 void* fence = nullptr, int flk = 0) {
     TileMap tm{};
     tm.ntiles = (n + (1 << LT) - 1) >> LT;
     if (p.kind == KIND_TILE_SORT) {
         if constexpr (sizeof(K) == 8) {
-            if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s);
-            else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
+            if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s, fence, flk);
+            else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s, fence, flk);
         } else if (LT == 15 && MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 10 && plan_knobs().sort_u32) {
-            launch_sort_u32(src, dst, n, s, fence, flk);
+            launch_sort_u32(src, dst, n, s, (uint64_t*)fence, flk);
         } else {
             launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s);
         }
@@ -1469,9 +1476,10 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
     const K* src = in;
     int fence_phase = 0;  // multi-way passes: fence buffer holding the next pass's fences
     // the u32 SORT pass writes the first multi-way pass's fences (no gather pass)
-    const bool sort_fences = sizeof(K) == 4 && LT == 15 && np > 1 && ps[0].kind == KIND_TILE_SORT &&
-                             ps[1].kind == KIND_RUNSK && ps[1].hi == LT && sort_u32_path() &&
-                             !(io && io->before_first);
+    // (u32: k_sort_u32 with the 2^15 tile; u64: the k_stream SORT tile)
+    const bool sort_fences = np > 1 && ps[0].kind == KIND_TILE_SORT && ps[1].kind == KIND_RUNSK &&
+                             ps[1].hi == LT && !(io && io->before_first) &&
+                             (sizeof(K) == 8 || (LT == 15 && sort_u32_path()));
     for (int i = 0; i < np; ++i) {
         // ping-pong: pass i writes `out` iff an even number of passes follow it
         K* dst = (!pp || ((np - 1 - i) & 1) == 0) ? out : scratch;
@@ -1509,7 +1517,7 @@ hipError_t local_sort_lt(const K* in, K* out, int64_t n, bool ord_in, K* scratch
             const hipError_t e = merge_level<K>(src, dst, n, p.hi, s);
             if (e != hipSuccess) return e;
         } else if (i == 0 && sort_fences) {
-            uint64_t* f = (uint64_t*)mergek_fence_buffer(n, (int)sizeof(K), 0, s);
+            void* f = mergek_fence_buffer(n, (int)sizeof(K), 0, s);
             if (!f) return hipErrorOutOfMemory;
             launch_pass<K, LT, LTR>(src, dst, n, p, ord_in, s, f, ps[1].R);
         } else {
