@@ -268,10 +268,15 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 // its lanes read that range coalesced and add each fence to its chunk's
 // counters in LDS (8-bit fields, runs 0..7 and 8..15 in two u64 words;
 // one lane per chunk reading its own FM fences ran 49 us at 2^30).
-// lanes of a fence-count block (SCAN_NT chunks): 1024 measured slower (46.8
-// vs 41.5 us at 2^30: the lanes of a wave add to the same few chunk counters)
-constexpr int COUNT_NT = SCAN_NT;
-template <typename FT>
+// Two ways to count, chosen by size: SLICES (few blocks, small sorts): each
+// of COUNT_NT lanes counts a contiguous slice of the block's fences in
+// registers and adds to a chunk's LDS counters when its slice crosses into
+// the next chunk -- 2^24: 32 -> 13 us per pass, where 10 blocks had walked 56
+// fences per lane; else (many blocks) the block's SCAN_NT lanes read the fence
+// range coalesced and add each fence to its chunk's counters with an LDS
+// atomic -- 2^30: 41.5 us, the slices' strided loads 107 us.
+constexpr int COUNT_NT = 1024;
+template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
                                                            int* __restrict__ P, int* __restrict__ bsum) {
     __shared__ uint64_t sws[COUNT_NT / 64];
@@ -289,12 +294,40 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     chunk_place(geo, c1 - 1, g, t);
     const int64_t gf = geo.base(g) >> FG_LOG2, nfg = geo.nfences(g);
     const int64_t f1 = t * geo.fm + geo.fm < nfg ? gf + t * geo.fm + geo.fm : gf + nfg;
-    for (int64_t e = f0 + tid; e < f1; e += COUNT_NT) {
-        int64_t ge = (e << FG_LOG2) >> gl;  // the fence's group (the tail group starts at nfull)
+    auto chunk_of = [&](int64_t e) {  // block-local chunk of fence e (the tail group starts at nfull)
+        int64_t ge = (e << FG_LOG2) >> gl;
         ge = ge < geo.nfull ? ge : geo.nfull;
-        const int64_t ce = ge * geo.kf + (e - (geo.base(ge) >> FG_LOG2)) / geo.fm;
-        const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
-        atomicAdd(&sc[ce - c0][r >> 3], 1ull << (8 * (r & 7)));
+        return ge * geo.kf + (e - (geo.base(ge) >> FG_LOG2)) / geo.fm - c0;
+    };
+    if constexpr (SLICES) {
+        const int64_t per = (f1 - f0 + COUNT_NT - 1) / COUNT_NT;
+        const int64_t e0 = f0 + tid * per, e1 = e0 + per < f1 ? e0 + per : f1;
+        int64_t cur = -1;  // the chunk being counted
+        uint64_t lo8 = 0, hi8 = 0;
+        for (int64_t e = e0; e < e1; ++e) {
+            const int64_t ce = chunk_of(e);
+            if (ce != cur) {
+                if (cur >= 0) {
+                    if (lo8) atomicAdd(&sc[cur][0], lo8);
+                    if (hi8) atomicAdd(&sc[cur][1], hi8);
+                }
+                cur = ce;
+                lo8 = hi8 = 0;
+            }
+            const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
+            const uint64_t one = 1ull << (8 * (r & 7));
+            if (r < 8) lo8 += one;
+            else hi8 += one;
+        }
+        if (cur >= 0) {
+            if (lo8) atomicAdd(&sc[cur][0], lo8);
+            if (hi8) atomicAdd(&sc[cur][1], hi8);
+        }
+    } else if (tid < SCAN_NT) {
+        for (int64_t e = f0 + tid; e < f1; e += SCAN_NT) {
+            const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
+            atomicAdd(&sc[chunk_of(e)][r >> 3], 1ull << (8 * (r & 7)));
+        }
     }
     __syncthreads();
     // scan 4 runs at a time as 16-bit fields of one u64 (block prefixes <=
@@ -888,7 +921,9 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         }
     }
     const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
-    k_fence_counts<FT><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
+    if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
     k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots,
                                                                           bounds);
