@@ -86,8 +86,11 @@ struct PlanKnobs {
     // in-LDS level and 16-way planning cost more than the pass they save)
     int multiway = 3;
     // the same for u64 (and f64) keys (MISORT_MULTIWAY_U64): 128-bit fences,
-    // 8192-key chunks at 2 workgroups per CU
-    int multiway_u64 = 3;
+    // 8192-key chunks at 2 workgroups per CU.  16-way passes measured faster
+    // for u64 at every size (profiles/r02/ab_mw: 2^24 +8 %, 2^26 +4 %, 2^27
+    // +1.5 %, 2^29 +2.5 % over 8-way): fewer passes, and u64 chains cost less
+    // per byte than u32 ones
+    int multiway_u64 = 4;
     PlanKnobs();
     int multiway_cap(int kb) const { return kb == 4 ? multiway : multiway_u64; }
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }

@@ -207,7 +207,7 @@ ctx.close()
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_NT": "512"}, (1 << 20) + 5),
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "0"}, (1 << 21) + 4099),  # 2-way passes
     (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "2"}, (1 << 21) + 4099),
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "4"}, (1 << 22) + 3),
+    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "3"}, (1 << 22) + 3),
     (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 25) + 12345),  # chained 8-way passes, u128 fence merges
 ])
 def test_full_sort_merge_from(kb, env, n):
@@ -218,7 +218,7 @@ def test_full_sort_merge_from(kb, env, n):
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
     _, count, _, countk, verdict = line.split()
     assert verdict == "OK", line
-    cap = int(env.get("MISORT_MULTIWAY" if kb == 4 else "MISORT_MULTIWAY_U64", "3"))
+    cap = int(env.get("MISORT_MULTIWAY", "3") if kb == 4 else env.get("MISORT_MULTIWAY_U64", "4"))
     if cap >= 2 and int(count) >= 2:
         assert int(countk) == -(-int(count) // cap)  # the fewest multi-way passes
     else:

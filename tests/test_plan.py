@@ -137,13 +137,14 @@ def test_plan_pass_counts():
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
     assert len(misort.plan(1 << 23, 4)) == 13  # cache-resident u32 sizes stay on the network
     assert [q[0] for q in misort.plan(1 << 24, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^24: 3 x 8-way
-    # u64: 2^13-key SORT tiles, then 16 levels in six multi-way passes
+    # u64: 2^13-key SORT tiles, then 16 levels in four 16-way passes
     # (128-bit fences; 2-way passes would be 1 + 16)
     p29 = misort.plan((1 << 29) - 3, 8)
-    assert p29[0][0] == KIND_SORT and [q[0] for q in p29[1:]] == [KIND_RUNSK] * 6
-    assert [q[2] for q in p29[1:]] == [3, 3, 3, 3, 2, 2]
+    assert p29[0][0] == KIND_SORT and [q[0] for q in p29[1:]] == [KIND_RUNSK] * 4
+    assert [q[2] for q in p29[1:]] == [4, 4, 4, 4]
+    assert [q[2] for q in misort.plan(1 << 26, 8)[1:]] == [4, 3, 3, 3]
     # a u64 multi-way pass ends at 2^29 at most (32-bit row offsets of 8-byte keys)
-    assert [q[0] for q in misort.plan(1 << 30, 8)] == [KIND_SORT] + [KIND_RUNSK] * 6 + [KIND_RUNS]
+    assert [q[0] for q in misort.plan(1 << 30, 8)] == [KIND_SORT] + [KIND_RUNSK] * 4 + [KIND_RUNS]
     assert [q[0] for q in misort.plan(1 << 14, 8)] == [KIND_SORT, KIND_RUNS]  # one level: 2-way
 
 
