@@ -228,6 +228,51 @@ def test_baseline_size_u32(ctx, logn):
     # fixtures are in test_gpu_baseline_configs.py
 
 
+def _multiset_props64(t):
+    """Order-independent fingerprint of a u64 tensor: sum, sum of squares (both
+    mod 2^64), xor of all keys, 2^16-bucket histogram of the top bits."""
+    v = t.view(torch.int64)
+    x = v.clone()
+    while x.numel() > 1:  # xor-reduce by halves (no torch xor reduction)
+        h = x.numel() // 2
+        y = x[:h] ^ x[h:2 * h]
+        x = torch.cat([y, x[2 * h:]]) if x.numel() % 2 else y
+    hist = torch.bincount(((v >> 48) & 0xFFFF).to(torch.int64), minlength=65536)
+    return int(v.sum()), int((v * v).sum()), int(x[0]), hist.cpu()
+
+
+def test_past_the_multiway_limit_u32(ctx):
+    """2^31 - 3 u32 keys: five 8-way passes end at runs of 2^30 (32-bit row
+    offsets), one 2-way pass merges the last level; ragged tail."""
+    n = (1 << 31) - 3
+    plan = misort.plan(n, 4)
+    assert [p[0] for p in plan][-2:] == ["run_mergek", "run_merge"]
+    d_in = torch.empty(n, dtype=U32_T, device="cuda")
+    ctx.fill_splitmix(d_in, 0x5EED0031)
+    d_out = torch.empty_like(d_in)
+    ctx.local_sort(d_in, d_out)
+    torch.cuda.synchronize()
+    assert ctx.check_sort(d_out) == 0
+    a, b = _multiset_props(d_in), _multiset_props(d_out)
+    assert a[:2] == b[:2] and torch.equal(a[2], b[2])
+
+
+def test_past_the_multiway_limit_u64(ctx):
+    """2^30 + 5 u64 keys: four 16-way passes end at runs of 2^29, two 2-way
+    passes follow; ragged tail."""
+    n = (1 << 30) + 5
+    plan = misort.plan(n, 8)
+    assert [p[0] for p in plan][-3:] == ["run_mergek", "run_merge", "run_merge"]
+    d_in = torch.empty(n, dtype=U64_T, device="cuda")
+    ctx.fill_splitmix(d_in, 0x5EED0064)
+    d_out = torch.empty_like(d_in)
+    ctx.local_sort(d_in, d_out)
+    torch.cuda.synchronize()
+    assert ctx.check_sort(d_out) == 0
+    a, b = _multiset_props64(d_in), _multiset_props64(d_out)
+    assert a[:3] == b[:3] and torch.equal(a[3], b[3])
+
+
 def test_f64_signed_zeros_total_order(ctx):
     """-0.0 == +0.0 as doubles: std::sort (psort.cc:175) leaves their relative
     order unspecified and compare_split keeps whichever side its '<'/'>' picks,
