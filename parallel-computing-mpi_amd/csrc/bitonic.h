@@ -82,9 +82,12 @@ struct PlanKnobs {
     int merge_min_log2_u32 = 23;
     // u32 merge levels: up to this many levels per multi-way pass (runsk.hip,
     // 2^lk-way, lk <= 4); 0 or 1: one 2-way pass per level (MISORT_MULTIWAY).
-    // 3 measured best at 2^30: 63.8 Gkeys/s vs 62.6 with 16-way passes (a 4th
-    // in-LDS level and 16-way planning cost more than the pass they save)
-    int multiway = 3;
+    // -1 (default): 3 when the L levels past the SORT tile are a multiple of
+    // 3 (then 8-way passes only), else 4 (the fewest passes) -- measured per
+    // size (profiles/r02/ab_mw_u32): L = 15 (2^30) 8-way 64.1 vs 63.2 Gkeys/s
+    // with 16-way, L = 12 63.5 vs 63.2; L = 10, 11, 13, 14 the fewer passes
+    // win by 4 / 3 / 1.6 / 0.7 %
+    int multiway = -1;
     // the same for u64 (and f64) keys (MISORT_MULTIWAY_U64): 128-bit fences,
     // 8192-key chunks at 2 workgroups per CU.  16-way passes measured faster
     // for u64 at every size (profiles/r02/ab_mw: 2^24 +8 %, 2^26 +4 %, 2^27
@@ -92,7 +95,12 @@ struct PlanKnobs {
     // per byte than u32 ones
     int multiway_u64 = 4;
     PlanKnobs();
-    int multiway_cap(int kb) const { return kb == 4 ? multiway : multiway_u64; }
+    // the cap for L levels
+    int multiway_cap(int kb, int L) const {
+        if (kb != 4) return multiway_u64;
+        if (multiway >= 0) return multiway;
+        return L % 3 == 0 ? 3 : 4;
+    }
     int merge_from(int kb) const { return kb == 4 ? merge_from_u32 : merge_from_u64; }
     // per key type: the large (128 KiB) SORT/MERGE and ROWS tiles, persistent modes
     bool big(int kb) const { return kb == 4 ? tile_u32 == 15 : tile_u64 == 14; }
@@ -1411,11 +1419,11 @@ std::vector<Pass> plan_uncached(int k, bool runs) {
         // 30 for u32, 13 and 29 for u64), the larger ones first; a single
         // level left over runs as a 2-way pass (which keeps host staging's
         // chunked final pass)
-        const int mw = kn.multiway_cap((int)sizeof(K));
         const int lwk_max = merge_levelk_lwk_max((int)sizeof(K));
+        const int L = (k < lwk_max ? k : lwk_max) - lw;  // levels the multi-way passes can take
+        const int mw = kn.multiway_cap((int)sizeof(K), L);
         if (mw >= 2 && lw >= merge_levelk_lw_min((int)sizeof(K))) {
             const int cap = mw < 4 ? mw : 4;
-            const int L = (k < lwk_max ? k : lwk_max) - lw;  // levels the multi-way passes can take
             if (L >= 2) {
                 const int np = (L + cap - 1) / cap;  // fewest passes
                 for (int i = 0; i < np; ++i) {

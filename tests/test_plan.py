@@ -130,9 +130,12 @@ def test_plan_pass_counts():
     p30 = misort.plan(1 << 30, 4)
     assert p30[0][0] == KIND_SORT
     assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 15 + 3 * i, 3) for i in range(5)]
-    # 13 and 14 levels: five passes, the levels spread 3,3,3,2,2 / 3,3,3,3,2
-    assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [3, 3, 3, 2, 2]
-    assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [3, 3, 3, 3, 2]
+    # 13 and 14 levels: four passes, one or two of them 16-way (fewer passes win
+    # unless the levels split into 8-way passes exactly); 12 levels: four 8-way
+    assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [4, 3, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [4, 4, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 27, 4)[1:]] == [3, 3, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 25, 4)[1:]] == [4, 3, 3]
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
     assert len(misort.plan(1 << 23, 4)) == 13  # cache-resident u32 sizes stay on the network
