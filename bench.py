@@ -410,8 +410,8 @@ def main(argv=None):
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys), then multi-way merge passes: up to 3 "
-                      "merge levels per HBM pass (8-way, runsk.hip; u64 with 128-bit fences) "
+        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys), then multi-way merge passes: 3-4 "
+                      "merge levels per HBM pass (8/16-way, runsk.hip; u64 with 128-bit fences) "
                       "(the reference's local std::sort, psort.cc:175)")
         out = {
             "metric": METRIC,
