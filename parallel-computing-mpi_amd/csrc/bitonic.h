@@ -442,6 +442,10 @@ __device__ __forceinline__ void sort_levels_w(K* s, int t) {
 #ifndef MISORT_SORT_TOP
 #define MISORT_SORT_TOP 15
 #endif
+// Probe-only (tools/build_variant.sh): last level the u64 SORT tile's LDS phases run.
+#ifndef MISORT_SORT_TOP_U64
+#define MISORT_SORT_TOP_U64 99
+#endif
 #ifndef MISORT_WAVE_SORT
 #define MISORT_WAVE_SORT 1
 #endif
@@ -856,7 +860,7 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
                 }
                 if constexpr (MISORT_SORT_WAVE_SYNC) wave_sync();  // level 6 stays inside the wave
                 else __syncthreads();
-                sort_levels_w<K, 6, LT>(s, t);
+                sort_levels_w<K, 6, (sizeof(K) == 8 && MISORT_SORT_TOP_U64 < LT ? MISORT_SORT_TOP_U64 : LT)>(s, t);
             } else {
                 lds_range_w<K, P.T_HI, P.T_LO, false, (P.H_HI >= P.H_LO ? P.H_HI : -1)>(s, t);
                 lds_range_w<K, P.H_HI, P.H_LO, true, -1>(s, t);
