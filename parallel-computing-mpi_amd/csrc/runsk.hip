@@ -396,7 +396,8 @@ __device__ __forceinline__ int64_t interp(KEY v, KEY ka, KEY kb, int64_t a, int6
 template <typename KEY>
 __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
                          const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
-                         const int* __restrict__ bsum, Geo geo, int64_t nslots, int64_t* __restrict__ bounds) {
+                         const int* __restrict__ bsum, Geo geo, int64_t nslots, int64_t* __restrict__ bounds,
+                         bool line) {
     typedef typename KTr<KEY>::F FT;
     const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= (nslots << geo.lk)) return;
@@ -462,9 +463,48 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
     }
     p = p < a ? a : (p > b ? b : p);
     int64_t lo_b, hi_b;  // the answer lies in [lo_b, hi_b]
-    if (p < b && before(p)) {
+    // line: first the guess's aligned 128-byte line in one round of vector
+    // loads: on spread keys it usually holds the answer (a count of the keys
+    // before it); otherwise it narrows the range to one side.  It cuts the
+    // dependent probe rounds, which pays when many searches share the memory
+    // system; a few thousand latency-bound ones run faster without it.
+    constexpr int BW = 128 / (int)sizeof(KEY);
+    const int64_t blk = (p < b ? p : b - 1) & ~(int64_t)(BW - 1);
+    bool fwd;
+    if (line && a < b && blk + BW <= len && ((uintptr_t)kr & 15) == 0) {
+        kvec<KEY> q[BW * (int)sizeof(KEY) / 16];
+#pragma unroll
+        for (int i = 0; i < BW * (int)sizeof(KEY) / 16; ++i) q[i] = reinterpret_cast<const kvec<KEY>*>(kr + blk)[i];
+        const int64_t l0 = blk > a ? blk : a, l1 = blk + BW < b ? blk + BW : b;
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < BW; ++i) {
+            const KEY k = q[i / (16 / (int)sizeof(KEY))][i % (16 / (int)sizeof(KEY))];
+            c += (blk + i >= l0 && blk + i < l1 && (le ? k <= v : k < v)) ? 1 : 0;
+        }
+        if (c > 0 && c < l1 - l0) {
+            bounds[id] = l0 + c;
+            return;
+        }
+        if (c == 0) {  // the answer is at or before l0
+            lo_b = a;
+            hi_b = l0;
+            fwd = false;
+        } else {  // after all of the line's keys in [a, b)
+            lo_b = l1;
+            hi_b = b;
+            fwd = true;
+        }
+    } else if (p < b && before(p)) {
         lo_b = p + 1;
         hi_b = b;
+        fwd = true;
+    } else {
+        lo_b = a;
+        hi_b = p;
+        fwd = false;
+    }
+    if (fwd) {
         for (int64_t step = 4;; step <<= 1) {
             const int64_t x = lo_b + step - 1;
             if (x >= hi_b) break;
@@ -476,8 +516,6 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
             }
         }
     } else {
-        lo_b = a;
-        hi_b = p;
         for (int64_t step = 4;; step <<= 1) {
             const int64_t x = hi_b - step;
             if (x < lo_b) break;
@@ -517,103 +555,100 @@ struct alignas(128) Desc {  // whole 128-byte lines: a chunk's entries never sha
     uint32_t la[Shape<KEY, LK>::NROWS];   // real keys of the row (0..RW) | LDS slot of its first key << 16
 };
 
-// One wave per DESC_CPW consecutive chunks (DESC_CPB waves per workgroup):
-// K lanes read and check each chunk's bounds -- all the wave's bounds loads
-// first, then the chunks one by one -- every lane gets them by shuffles, then
-// the lanes write the table entries.
-constexpr int DESC_CPB = 4, DESC_CPW = 4;
+// DC chunks per one-wave workgroup (16; 4 for small sorts, which then still
+// spread over many waves), in two phases.  Lane = chunk: read its 2K
+// bounds (one contiguous row), check them and prefix the segment lengths and
+// row counts into an LDS header, plus a row -> segment map.  Lane = table
+// entry: each (chunk, row) entry is computed from the header and stored, so
+// consecutive lanes write consecutive words of a descriptor.  (One lane per
+// chunk and entry keeps the instruction count at a few dozen per chunk; a wave
+// per chunk spent ~500, k_chunk_desc being bound by them.)
+constexpr int DC_NT = 64;
 
 template <typename KEY, int LK>
-__device__ __forceinline__ void desc_one(const Geo& geo, int64_t c, int64_t g, int lane, int64_t st, int64_t en,
-                                         Desc<KEY, LK>* __restrict__ desc) {
+struct DescHdr {
+    static constexpr int K = Shape<KEY, LK>::K;
+    int64_t gbase, out0;
+    int so[K + 1], srow[K + 1], sln[K];
+    uint32_t sb[K];
+};
+
+template <typename KEY, int LK, int DC>
+__global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo, int64_t nchunks,
+                                                   Desc<KEY, LK>* __restrict__ desc) {
     typedef Shape<KEY, LK> S;
-    constexpr int K = S::K;
-    const int64_t ln = en - st;
-    bool ok = true;
-    if (lane < K) ok = st >= 0 && ln >= 0 && en <= geo.run_len(g, lane) && ln <= S::CAP;
-    // bounds outside the runs would be a logic error: never let them address memory
-    ok = __all(ok);
-    // the K lanes' values as scalars (starts < W <= 2^28 and lengths <= CAP fit 32 bits)
-    int sln[K], sst[K];
-    int tot = 0;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        sln[r] = __builtin_amdgcn_readlane((int)ln, r);
-        sst[r] = __builtin_amdgcn_readlane((int)st, r);
-        tot += sln[r];
-    }
-    ok = ok && tot <= S::CAP;
-    int srow[K + 1], so[K + 1];
-    uint32_t sb[K];  // byte offset of segment r's first key from the group base (< KW*sizeof(KEY) <= 2^32)
-    int R = 0, o = 0;
-    int64_t out = geo.base(g);
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        if (!ok) sln[r] = sst[r] = 0;
-        srow[r] = R;
-        so[r] = o;
-        sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)sst[r]) * (uint32_t)sizeof(KEY);
-        R += (sln[r] + S::RW - 1) / S::RW;
-        o += sln[r];
-        out += sst[r];
-    }
-    srow[K] = R;
-    so[K] = o;
-    Desc<KEY, LK>& d = desc[c];
-    if (lane == 0) {
-        d.gbase = geo.base(g);
-        d.out0 = out;
-    }
-#pragma unroll
-    for (int r = 0; r <= K; ++r)
-        if (lane == r) d.o[r] = so[r];
-    for (int j = lane; j < S::NROWS; j += 64) {
-        const int row = (j % S::IT) * S::NR + j / S::IT;  // table entry j (stored by part)
-        // the row's segment: the last one starting at or before it
-        int rr = 0;
-#pragma unroll
-        for (int r = 1; r < K; ++r) rr = row >= srow[r] ? r : rr;
-        int rs = 0, rl = 0, rb = 0;
-        uint32_t ro = 0;
+    constexpr int K = S::K, NROWS = S::NROWS;
+    __shared__ DescHdr<KEY, LK> hdr[DC];
+    __shared__ uint8_t seg[DC][NROWS];  // row -> its segment
+    const int lane = threadIdx.x;
+    const int64_t cb = (int64_t)blockIdx.x * DC;
+    const int nc = nchunks - cb < DC ? (int)(nchunks - cb) : DC;
+    if (lane < nc) {
+        int64_t g, t;
+        chunk_place(geo, cb + lane, g, t);
+        const int64_t* b0 = bounds + K * geo.slot(g, t);
+        int64_t st[K], en[K];
 #pragma unroll
         for (int r = 0; r < K; ++r) {
-            if (rr == r) {
-                rs = srow[r];
-                rl = sln[r];
-                rb = so[r] + r * S::G;
-                ro = sb[r];
-            }
+            st[r] = b0[r];
+            en[r] = b0[K + r];
         }
-        const int k = row - rs, rem = rl - k * S::RW;
-        const bool in = row < srow[K];  // rows past the chunk: no keys
-        d.off[j] = in ? ro + (uint32_t)(k * S::RW * (int)sizeof(KEY)) : 0u;
-        d.la[j] = in ? (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(rb + k * S::RW) << 16) : 0u;
-    }
-}
-
-template <typename KEY, int LK>
-__global__ __launch_bounds__(64 * DESC_CPB) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo,
-                                                             int64_t nchunks, Desc<KEY, LK>* __restrict__ desc) {
-    constexpr int K = Shape<KEY, LK>::K;
-    const int64_t c0 = ((int64_t)blockIdx.x * DESC_CPB + (threadIdx.x >> 6)) * DESC_CPW;
-    const int lane = threadIdx.x & 63;
-    int64_t g[DESC_CPW], st[DESC_CPW], en[DESC_CPW];
+        // bounds outside the runs would be a logic error: never let them address memory
+        bool ok = true;
+        int64_t tot = 0;
 #pragma unroll
-    for (int i = 0; i < DESC_CPW; ++i) {
-        st[i] = en[i] = g[i] = 0;
-        if (c0 + i < nchunks) {  // whole waves
-            int64_t t;
-            chunk_place(geo, c0 + i, g[i], t);
-            const int64_t* b0 = bounds + K * geo.slot(g[i], t);
-            if (lane < K) {
-                st[i] = b0[lane];
-                en[i] = b0[K + lane];
-            }
+        for (int r = 0; r < K; ++r) {
+            const int64_t ln = en[r] - st[r];
+            ok = ok && st[r] >= 0 && ln >= 0 && en[r] <= geo.run_len(g, r) && ln <= S::CAP;
+            tot += ln;
         }
-    }
+        ok = ok && tot <= S::CAP;
+        DescHdr<KEY, LK>& h = hdr[lane];
+        int R = 0, o = 0;
+        int64_t out = geo.base(g);
 #pragma unroll
-    for (int i = 0; i < DESC_CPW; ++i)
-        if (c0 + i < nchunks) desc_one<KEY, LK>(geo, c0 + i, g[i], lane, st[i], en[i], desc);
+        for (int r = 0; r < K; ++r) {
+            const int ln = ok ? (int)(en[r] - st[r]) : 0, s0 = ok ? (int)st[r] : 0;
+            h.srow[r] = R;
+            h.so[r] = o;
+            h.sln[r] = ln;
+            // byte offset of segment r's first key from the group base (< KW*sizeof(KEY) <= 2^32)
+            h.sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)s0) * (uint32_t)sizeof(KEY);
+            const int nr = (ln + S::RW - 1) / S::RW;
+            for (int q = 0; q < nr; ++q) seg[lane][R + q] = (uint8_t)r;
+            R += nr;
+            o += ln;
+            out += s0;
+        }
+        h.srow[K] = R;
+        h.so[K] = o;
+        h.gbase = geo.base(g);
+        h.out0 = out;
+    }
+    __syncthreads();
+    Desc<KEY, LK>* d = desc + cb;
+    for (int e = lane; e < nc * NROWS; e += DC_NT) {
+        const int cl = e / NROWS, j = e - cl * NROWS;
+        const DescHdr<KEY, LK>& h = hdr[cl];
+        const int row = (j % S::IT) * S::NR + j / S::IT;  // table entry j (stored by part)
+        uint32_t off = 0, la = 0;
+        if (row < h.srow[K]) {  // rows past the chunk: no keys
+            const int rr = seg[cl][row];
+            const int k = row - h.srow[rr], rem = h.sln[rr] - k * S::RW;
+            off = h.sb[rr] + (uint32_t)(k * S::RW * (int)sizeof(KEY));
+            la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(h.so[rr] + rr * S::G + k * S::RW) << 16);
+        }
+        d[cl].off[j] = off;
+        d[cl].la[j] = la;
+    }
+    for (int e = lane; e < nc * (K + 1); e += DC_NT) {
+        const int cl = e / (K + 1), r = e - cl * (K + 1);
+        d[cl].o[r] = hdr[cl].so[r];
+    }
+    if (lane < nc) {
+        d[lane].gbase = hdr[lane].gbase;
+        d[lane].out0 = hdr[lane].out0;
+    }
 }
 
 // Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
@@ -925,11 +960,13 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
+    // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
+    static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
+    static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
     k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots,
-                                                                          bounds);
-    k_chunk_desc<KEY, LK>
-        <<<(unsigned)((nchunks + DESC_CPB * DESC_CPW - 1) / (DESC_CPB * DESC_CPW)), 64 * DESC_CPB, 0, s>>>(
-            bounds, geo, nchunks, desc);
+                                                                          bounds, (nslots << LK) >= line_min);
+    if (nchunks >= dc16_min) k_chunk_desc<KEY, LK, 16><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
+    else k_chunk_desc<KEY, LK, 4><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
     const unsigned grid = (unsigned)nchunks;
     if (hook) hook->before(KIND_RUNSK_KERNEL, 2.0 * (double)n * sizeof(KEY), s);
     if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);

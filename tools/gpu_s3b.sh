@@ -1,0 +1,18 @@
+# Session-3: A/B of the planning kernels on one box: new (in-tree) vs old (lib/variants/libmisort_old.so),
+# alternating, u32 2^24..2^30 and u64 2^26/2^29; merge tests first.
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${OUTDIR:-s3b}"; mkdir -p "$O"; cd "$R"
+fatal() { case "$1" in 124|137|134|139) echo "fatal rc $1 in $2: stopping"; exit "$1";; esac; }
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_runs.py -x -q --timeout 300 --timeout-method thread \
+  > "$O/pytest.log" 2>&1; rc=$?; echo "pytest rc $rc"; tail -2 "$O/pytest.log"; fatal $rc pytest; [ $rc -ne 0 ] && exit $rc
+one() {  # tag lib dtype logn
+  MISORT_LIBRARY=$2 timeout -k 10 200 python3 -u bench.py --dtype $3 --logn $4 --steps 20 --warmup 5 --no-cpu-baseline > "$O/$1_$3_$4.json" 2> "$O/$1_$3_$4.err"; rc=$?
+  fatal $rc "bench $1 $3 $4"; [ $rc -ne 0 ] && exit $rc
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1].split('/')[-1], round(d['value'],2), round(d['ms_per_step'],4), d['check_errors'])" "$O/$1_$3_$4.json"
+}
+NEW="$R/parallel-computing-mpi_amd/lib/libmisort.so"; OLD="$R/parallel-computing-mpi_amd/lib/variants/libmisort_old.so"
+for rep in 1 2; do
+  for L in 24 26 28 30; do one new$rep $NEW u32 $L; one old$rep $OLD u32 $L; done
+  for L in 26 29; do one new$rep $NEW u64 $L; one old$rep $OLD u64 $L; done
+done
+exit 0
