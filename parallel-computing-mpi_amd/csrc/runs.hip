@@ -9,8 +9,8 @@
 // keys carry no payload, so every correct sort of them writes the same bytes.
 //
 // Per level, two launches:
-//   k_runs_partition  one lane per output tile: the merge-path co-rank of the
-//                     tile's first output within its pair (binary search, A
+//   k_runs_partition  32 lanes per output tile: the merge-path co-rank of the
+//                     tile's first output within its pair (a 32-ary search, A
 //                     first on ties);
 //   k_runs_merge      one workgroup per output tile of NT*IT keys: its A and B
 //                     ranges are streamed into LDS, each lane finds its own
@@ -84,29 +84,39 @@ __device__ __forceinline__ PairGeo pair_geo(int64_t g, int64_t n, int lw) {
     return PairGeo{base, na, nb};
 }
 
-// Number of A keys among the first d outputs of merge(A, B), A first on ties.
-template <typename K>
-__device__ int64_t run_corank(const K* __restrict__ A, int64_t na, const K* __restrict__ B, int64_t nb,
-                              int64_t d) {
-    int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (A[mid] <= B[d - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
+// co[i] = the number of A keys among the first d outputs of merge(A, B), A
+// first on ties, for the first output d of tile t0 + i within its pair.
+// One group of PART_LANES lanes per tile start: each round the lanes evaluate
+// the co-rank predicate (A[x] <= B[d-1-x]: true, then false) at PART_LANES
+// evenly spaced points of the bracket and keep the step around the first
+// false one -- ceil(log32(range)) dependent rounds of loads instead of
+// log2(range) (a 2^23-key pair: 5 instead of 23; the kernel is a chain of
+// load latencies).
+constexpr int PART_LANES = 32;
 
 template <typename K, int NT, int IT>
-__global__ void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, int64_t t0, int64_t ntiles,
-                                 int64_t* __restrict__ co) {
+__global__ __launch_bounds__(256) void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, int64_t t0,
+                                                        int64_t ntiles, int64_t* __restrict__ co) {
     constexpr int TILE = NT * IT;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ntiles) return;
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / PART_LANES;
+    const int sub = (int)(threadIdx.x % PART_LANES), shift = (int)(threadIdx.x & 63) & ~(PART_LANES - 1);
+    if (i >= ntiles) return;  // whole lane groups
     const int64_t g0 = (t0 + i) * TILE;
     const PairGeo p = pair_geo(g0, n, lw);
     const K* A = src + p.base;
-    co[i] = run_corank(A, p.na, A + ((int64_t)1 << lw), p.nb, g0 - p.base);
+    const K* B = A + ((int64_t)1 << lw);
+    const int64_t d = g0 - p.base;
+    int64_t lo = d > p.nb ? d - p.nb : 0, hi = d < p.na ? d : p.na;
+    while (lo < hi) {
+        const int64_t step = (hi - lo + PART_LANES - 1) / PART_LANES;
+        const int64_t x = lo + sub * step;
+        const bool t = x < hi && A[x] <= B[d - 1 - x];
+        const int c = __popc((uint32_t)(__ballot(t) >> shift));  // the true points are a prefix
+        const int64_t nhi = lo + c * step;
+        lo = c > 0 ? lo + (c - 1) * step + 1 : lo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    if (sub == 0) co[i] = lo;
 }
 
 template <typename K, int NT, int IT>
@@ -235,7 +245,7 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
     const int64_t nco = t0 + ntiles < (n + TILE - 1) / TILE ? ntiles + 1 : ntiles;
     int64_t* co = corank_scratch((size_t)(ntiles + 1) * sizeof(int64_t), s);
     if (!co) return hipErrorOutOfMemory;
-    k_runs_partition<K, NT, IT><<<(unsigned)((nco + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
+    k_runs_partition<K, NT, IT><<<(unsigned)((nco * PART_LANES + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
     k_runs_merge<K, NT, IT><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, co);
     return hipGetLastError();
 }
