@@ -197,20 +197,24 @@ __global__ void k_fence_gather(const KEY* __restrict__ src, int64_t n, int lw, i
 }
 
 // Runs of 2^wf fences merged 2^a at a time (<= 64 KiB of fences) into total
-// order in LDS: block b takes fences [b << (wf + a), ...); each fence's rank =
-// its index in its run's list + its lower bound in the sub-group's other runs.
+// order in LDS: blocks b*split .. b*split + split - 1 take fences
+// [b << (wf + a), ...), each ranking a 1/split slice of them (small sorts: more
+// blocks than sub-groups); each fence's rank = its index in its run's list +
+// its lower bound in the sub-group's other runs.
 template <typename FT>
 __global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT* __restrict__ M, int64_t nf,
-                                                    int wf_log2, int a) {
+                                                    int wf_log2, int a, int split) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sraw[];
     FT* sf = reinterpret_cast<FT*>(sraw);
-    const int64_t f0 = (int64_t)blockIdx.x << (wf_log2 + a);
+    const int64_t f0 = (int64_t)(blockIdx.x / split) << (wf_log2 + a);
     const int nfg = (int)((nf - f0) < ((int64_t)1 << (wf_log2 + a)) ? nf - f0 : ((int64_t)1 << (wf_log2 + a)));
     const int wf = 1 << wf_log2;
     const int K = 1 << a;
     for (int e = threadIdx.x; e < nfg; e += blockDim.x) sf[e] = F[f0 + e];
     __syncthreads();
-    for (int e = threadIdx.x; e < nfg; e += blockDim.x) {
+    const int sl = (nfg + split - 1) / split, e0 = (int)(blockIdx.x % split) * sl;
+    const int e1 = e0 + sl < nfg ? e0 + sl : nfg;
+    for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
         const FT v = sf[e];
         const int r = e / wf;
         int rank = e - r * wf;
@@ -231,9 +235,11 @@ __global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT
 }
 
 // Chunk index -> (group, chunk within the group), and the group's first chunk.
+// Chunk and bounds-slot indices are < 2^31 (merge_pass checks), so the
+// divisions are 32-bit.
 __device__ __forceinline__ void chunk_place(const Geo& geo, int64_t c, int64_t& g, int64_t& t) {
     if (c < geo.nfull * geo.kf) {
-        g = c / geo.kf;
+        g = (uint32_t)c / (uint32_t)geo.kf;
         t = c - g * geo.kf;
     } else {
         g = geo.nfull;
@@ -294,10 +300,15 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     chunk_place(geo, c1 - 1, g, t);
     const int64_t gf = geo.base(g) >> FG_LOG2, nfg = geo.nfences(g);
     const int64_t f1 = t * geo.fm + geo.fm < nfg ? gf + t * geo.fm + geo.fm : gf + nfg;
-    auto chunk_of = [&](int64_t e) {  // block-local chunk of fence e (the tail group starts at nfull)
+    // block-local chunk of fence e (the tail group starts at nfull); a fence's
+    // index within its group (< 2^(LWK_MAX - FG_LOG2)) and FM fit 32 bits, and a
+    // 32-bit division is a few VALU ops where a 64-bit one is ~100 (it bounded
+    // the kernel: one division per fence)
+    const uint32_t fm = (uint32_t)geo.fm;
+    auto chunk_of = [&](int64_t e) {
         int64_t ge = (e << FG_LOG2) >> gl;
         ge = ge < geo.nfull ? ge : geo.nfull;
-        return ge * geo.kf + (e - (geo.base(ge) >> FG_LOG2)) / geo.fm - c0;
+        return ge * geo.kf + (int64_t)((uint32_t)(e - (geo.base(ge) >> FG_LOG2)) / fm) - c0;
     };
     if constexpr (SLICES) {
         const int64_t per = (f1 - f0 + COUNT_NT - 1) / COUNT_NT;
@@ -405,7 +416,7 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
     const int r = (int)(id & (geo.K() - 1));
     int64_t g, t;
     if (s < geo.nfull * (geo.kf + 1)) {
-        g = s / (geo.kf + 1);
+        g = (uint32_t)s / (uint32_t)(geo.kf + 1);
         t = s - g * (geo.kf + 1);
     } else {
         g = geo.nfull;
@@ -911,7 +922,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const int64_t nchunks = chunks_of(geo);
     const int64_t nslots = geo.nfull * (geo.kf + 1) + (tail ? geo.nchunks(geo.nfull) + 1 : 0);
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
-    if (nchunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    if (nchunks >= ((int64_t)1 << 31) || nslots >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     // fence buffers 0 and 1 (kept across passes); per pass: merged fences,
     // fence merge temp, bounds, fence counts and their block totals, descriptors
     const int64_t nbk = (nchunks + SCAN_NT - 1) / SCAN_NT;
@@ -945,7 +956,10 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             FT* y = (left & 1) ? T : M;
             const size_t lds = ((size_t)1 << (wf_log2 + a)) * sizeof(FT);
             const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
-            k_fence_lds<FT><<<(unsigned)nb0, 1024, lds, s>>>(F, y, nf, wf_log2, a);
+            // >= 512 blocks where the sub-groups are few (each loads its whole sub-group)
+            int split = 1;
+            while (split < 8 && nb0 * split < 512 && ((int64_t)1 << (wf_log2 + a)) / (split * 2) >= 1024) split *= 2;
+            k_fence_lds<FT><<<(unsigned)(nb0 * split), 1024, lds, s>>>(F, y, nf, wf_log2, a, split);
             x = y;
         }
         for (int l = a; l < LK; ++l, --left) {
