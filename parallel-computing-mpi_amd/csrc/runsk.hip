@@ -284,12 +284,12 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 constexpr int COUNT_NT = 1024;
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
-                                                           int* __restrict__ P, int* __restrict__ bsum) {
+                                                           int cpb, int* __restrict__ P, int* __restrict__ bsum) {
     __shared__ uint64_t sws[COUNT_NT / 64];
     __shared__ unsigned long long sc[SCAN_NT][2];
     const int tid = threadIdx.x;
-    const int64_t c0 = (int64_t)blockIdx.x * SCAN_NT, c = c0 + tid;
-    const int64_t c1 = c0 + SCAN_NT < nchunks ? c0 + SCAN_NT : nchunks;
+    const int64_t c0 = (int64_t)blockIdx.x * cpb, c = c0 + tid;  // cpb <= SCAN_NT chunks per block
+    const int64_t c1 = c0 + cpb < nchunks ? c0 + cpb : nchunks;
     const int K = geo.K();
     const int gl = geo.lw + geo.lk;
     if (tid < SCAN_NT) sc[tid][0] = sc[tid][1] = 0ull;
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     __syncthreads();
     // scan 4 runs at a time as 16-bit fields of one u64 (block prefixes <=
     // SCAN_NT * FM < 2^16): K/4 block scans instead of K
-    const uint64_t w8[2] = {tid < SCAN_NT ? sc[tid][0] : 0ull, tid < SCAN_NT ? sc[tid][1] : 0ull};
+    const uint64_t w8[2] = {tid < cpb ? sc[tid][0] : 0ull, tid < cpb ? sc[tid][1] : 0ull};
     for (int q0 = 0; q0 < K; q0 += 4) {
         uint64_t v = 0;
 #pragma unroll
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
         for (int j = 0; j < nq; ++j) {
             const int q = q0 + j;
             const int vi = (int)((inc >> (16 * j)) & 0xFFFF), vq = (int)((v >> (16 * j)) & 0xFFFF);
-            if (tid < SCAN_NT && c < nchunks) P[c * K + q] = vi - vq;
+            if (tid < cpb && c < nchunks) P[c * K + q] = vi - vq;
             if (threadIdx.x == SCAN_NT - 1) bsum[(int64_t)blockIdx.x * K + q] = vi;
         }
     }
@@ -407,8 +407,8 @@ __device__ __forceinline__ int64_t interp(KEY v, KEY ka, KEY kb, int64_t a, int6
 template <typename KEY>
 __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
                          const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
-                         const int* __restrict__ bsum, Geo geo, int64_t nslots, int64_t* __restrict__ bounds,
-                         bool line) {
+                         const int* __restrict__ bsum, int cpb, Geo geo, int64_t nslots,
+                         int64_t* __restrict__ bounds, bool line) {
     typedef typename KTr<KEY>::F FT;
     const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= (nslots << geo.lk)) return;
@@ -441,8 +441,8 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
     // fences of run r before f: counts of the group's chunks before chunk t
     const int K = geo.K();
     const int64_t c = g * geo.kf + t, c0 = g * geo.kf;  // the tail group starts at nfull * kf too
-    const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / SCAN_NT) * K + r]) -
-                       (P[c0 * K + r] + bsum[(c0 / SCAN_NT) * K + r]);
+    const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / cpb) * K + r]) -
+                       (P[c0 * K + r] + bsum[(c0 / cpb) * K + r]);
     if (lo <= 0) {  // run r's first key comes after f
         bounds[id] = 0;
         return;
@@ -925,10 +925,14 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     if (nchunks >= ((int64_t)1 << 31) || nslots >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     // fence buffers 0 and 1 (kept across passes); per pass: merged fences,
     // fence merge temp, bounds, fence counts and their block totals, descriptors
-    const int64_t nbk = (nchunks + SCAN_NT - 1) / SCAN_NT;
+    // chunks per fence-count block: SCAN_NT, or fewer (down to 32) while that
+    // leaves under 128 blocks -- a small sort's few blocks walked long slices
+    int cpb = SCAN_NT;
+    while (cpb > 32 && (nchunks + cpb - 1) / cpb < 128) cpb /= 2;
+    const int64_t nbk = (nchunks + cpb - 1) / cpb;
     const size_t fb = ((size_t)nf * sizeof(FT) + 255) & ~(size_t)255;
     const size_t bb = ((size_t)nslots * S::K * 8 + 255) & ~(size_t)255;
-    const size_t cb = ((size_t)nbk * SCAN_NT * S::K * 4 + 255) & ~(size_t)255;
+    const size_t cb = ((size_t)nbk * cpb * S::K * 4 + 255) & ~(size_t)255;
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
     char* fbase = (char*)scratch(0, 2 * fb, s);
     char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
@@ -969,15 +973,15 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             x = y;
         }
     }
-    const int64_t nb = (nchunks + SCAN_NT - 1) / SCAN_NT;
+    const int64_t nb = nbk;
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
-    if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
-    else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cnt, bsum);
+    if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
+    else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
-    k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, geo, nslots,
+    k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo, nslots,
                                                                           bounds, (nslots << LK) >= line_min);
     if (nchunks >= dc16_min) k_chunk_desc<KEY, LK, 16><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
     else k_chunk_desc<KEY, LK, 4><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
