@@ -362,30 +362,46 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     }
 }
 
-// Exclusive scan of the block totals (one workgroup, carried over rounds),
-// two runs at a time as 32-bit fields of one u64 (totals < 2^31).
-__global__ __launch_bounds__(SCAN_NT) void k_scan_totals(int* __restrict__ bsum, int64_t nb, int K) {
-    __shared__ uint64_t sw[SCAN_NT / 64];
-    __shared__ uint64_t tot;
-    for (int q = 0; q < K; q += 2) {
-        const bool two = q + 1 < K;
-        uint64_t carry = 0;
-        for (int64_t b0 = 0; b0 < nb; b0 += SCAN_NT) {
-            const int64_t b = b0 + threadIdx.x;
-            const uint64_t v = b < nb ? (uint64_t)(uint32_t)bsum[b * K + q] |
-                                            (two ? (uint64_t)(uint32_t)bsum[b * K + q + 1] << 32 : 0ull)
-                                      : 0ull;
-            const uint64_t inc = block_scan_u64(v, sw);
-            const uint64_t ex = carry + inc - v;
+// Exclusive scan of the block totals: one wave per two runs (their totals as
+// the 32-bit fields of one u64; totals < 2^31), in rounds of 64 x TOT_B
+// blocks: a lane loads TOT_B consecutive totals at once, scans them in
+// registers, and a wave scan of the lane sums places them (one round of load
+// latency per 64 * TOT_B blocks; a 256-lane block scan per 256 blocks and run
+// pair took 4 dependent rounds per pair at 2^30).
+constexpr int TOT_B = 16;
+__global__ __launch_bounds__(512) void k_scan_totals(int* __restrict__ bsum, int64_t nb, int K) {
+    const int lane = threadIdx.x & 63, q = 2 * (int)(threadIdx.x >> 6);
+    if (q >= K) return;
+    const bool two = q + 1 < K;
+    uint64_t carry = 0;
+    for (int64_t r0 = 0; r0 < nb; r0 += 64 * TOT_B) {
+        const int64_t b0 = r0 + (int64_t)lane * TOT_B;
+        uint64_t v[TOT_B], sum = 0;
+#pragma unroll
+        for (int j = 0; j < TOT_B; ++j) {
+            const int64_t b = b0 + j;
+            v[j] = b < nb ? (uint64_t)(uint32_t)bsum[b * K + q] |
+                                (two ? (uint64_t)(uint32_t)bsum[b * K + q + 1] << 32 : 0ull)
+                          : 0ull;
+            sum += v[j];
+        }
+        uint64_t inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(inc, o, 64);
+            inc += lane >= o ? u : 0ull;
+        }
+        uint64_t ex = carry + inc - sum;
+#pragma unroll
+        for (int j = 0; j < TOT_B; ++j) {
+            const int64_t b = b0 + j;
             if (b < nb) {
                 bsum[b * K + q] = (int)(uint32_t)ex;
                 if (two) bsum[b * K + q + 1] = (int)(uint32_t)(ex >> 32);
             }
-            if (threadIdx.x == SCAN_NT - 1) tot = inc;
-            __syncthreads();
-            carry += tot;
-            __syncthreads();
+            ex += v[j];
         }
+        carry += __shfl(inc, 63, 64);
     }
 }
 
@@ -977,7 +993,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
     if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
-    k_scan_totals<<<1, SCAN_NT, 0, s>>>(bsum, nb, S::K);
+    k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
