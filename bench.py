@@ -214,15 +214,78 @@ def port_baseline(logn, why):
             "fallback_reason": why}
 
 
-def load_traffic(workload=None):
-    """Per-launch HBM bytes from committed rocprofv3 --pmc summaries (or None):
-    profiles/traffic_<workload>.json if present, else profiles/traffic.json."""
-    for name in ([f"traffic_{workload}.json"] if workload else []) + ["traffic.json"]:
-        p = os.path.join(ROOT, "profiles", name)
-        if os.path.exists(p):
-            with open(p) as f:
-                return json.load(f)
-    return None
+def load_traffic(workload):
+    """Per-launch HBM bytes of this exact workload from the committed rocprofv3
+    --pmc summary profiles/traffic_<workload>.json (tools/traffic.py), or None
+    -- never another workload's figures."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        t = json.load(f)
+    return t if t.get("workload") == workload else None
+
+
+LOCAL_KINDS = ("tile_sort", "global_pass", "tile_merge", "span_pass", "wide_pass", "run_merge", "run_mergek",
+               "run_mergek_kernel")
+
+
+def per_pass(trace, steps):
+    """The local sort's HBM passes of one step, averaged over the profiled
+    steps: [{"kind", "ms", "bytes", "kernel_ms"}] in pass order.  A multi-way
+    pass (run_mergek) carries its k_mergek launch (recorded just before it) as
+    kernel_ms; other passes are single kernels."""
+    recs = [r for r in trace if r[0] in LOCAL_KINDS]
+    if not recs or steps < 1 or len(recs) % steps:
+        return []
+    per = len(recs) // steps
+    rows = None
+    for st in range(steps):
+        out, held = [], None
+        for kind, ms, byt in recs[st * per:(st + 1) * per]:
+            if kind == "run_mergek_kernel":
+                held = ms
+                continue
+            out.append([kind, ms, byt, held if kind == "run_mergek" else None])
+            held = None
+        if rows is None:
+            rows = out
+        elif len(out) != len(rows) or any(a[0] != b[0] for a, b in zip(out, rows)):
+            return []  # steps differ in shape: no per-pass average
+        else:
+            for a, b in zip(rows, out):
+                a[1] += b[1]
+                a[2] = b[2]
+                if a[3] is not None:
+                    a[3] += b[3]
+    return [{"kind": k, "ms": ms / steps, "bytes": byt, "kernel_ms": None if km is None else km / steps}
+            for k, ms, byt, km in rows]
+
+
+def pass_rows(passes, traffic):
+    """roofline.passes: per-pass achieved rate and fraction of the HBM peak;
+    `traffic_ratio` = PMC bytes / algorithmic bytes of that pass when the
+    committed capture has per-pass figures for this workload."""
+    tp = (traffic or {}).get("passes") or []
+    if len(tp) != len(passes):
+        tp = [None] * len(passes)
+    rows = []
+    for i, (p, t) in enumerate(zip(passes, tp)):
+        ach = p["bytes"] / (p["ms"] * 1e-3) / 1e9 if p["ms"] > 0 else None
+        row = {"pass": i, "kind": p["kind"], "ms": p["ms"], "algorithmic_bytes": p["bytes"], "achieved": ach,
+               "frac": ach / HBM_PEAK_GBS if ach else None}
+        if p["kernel_ms"]:
+            kach = p["bytes"] / (p["kernel_ms"] * 1e-3) / 1e9
+            row["kernel"] = {"name": "k_mergek", "ms": p["kernel_ms"], "achieved": kach,
+                             "frac": kach / HBM_PEAK_GBS}
+        if t and t.get("kind") == p["kind"] and t.get("bytes"):
+            row["traffic"] = t["bytes"]
+            row["traffic_ratio"] = t["bytes"] / p["bytes"] if p["bytes"] else None
+            if t.get("kernel_bytes") and "kernel" in row:
+                row["kernel"]["traffic"] = t["kernel_bytes"]
+                row["kernel"]["traffic_ratio"] = t["kernel_bytes"] / p["bytes"]
+        rows.append(row)
+    return rows
 
 
 # -------------------------------------------------------------------- ranks
@@ -324,6 +387,7 @@ def main(argv=None):
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     kern = ctx.profile_read() if events else {}
+    passes = per_pass(ctx.profile_trace(), args.steps) if events else []
     nst = len(misort.schedule(nranks, rank))
     stages = ctx.profile_stages(nst) if events and nranks > 1 and args.algo == "bitonic" else []
     ctx.profile(False)
@@ -468,19 +532,22 @@ def main(argv=None):
             wl = f"{args.dtype}_2e{args.logn}_n{nranks}"
             traffic = load_traffic(wl)
             tr = None
-            if traffic and traffic.get("workload") == wl and name in traffic and \
-                    traffic[name].get("bytes_per_launch"):
+            if traffic and name in traffic and traffic[name].get("bytes_per_launch"):
                 tr = traffic[name]["bytes_per_launch"]
             achieved = byt / (tms * 1e-3) / 1e9
             out["roofline"] = {"kernel": name, "bound": "hbm", "achieved": achieved,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                                "traffic": tr, "algorithmic_bytes_per_launch": byt / nl,
-                               "avg_launch_us": tms / nl * 1e3}
+                               "avg_launch_us": tms / nl * 1e3,
+                               "traffic_source": (f"profiles/traffic_{wl}.json ({traffic.get('source')})"
+                                                  if traffic else None)}
+            if passes:
+                out["roofline"]["passes"] = pass_rows(passes, traffic)
             if name != fam:
                 pnl, pms, pbyt = kern[fam]
                 pach = pbyt / (pms * 1e-3) / 1e9
-                ptr = traffic[fam]["bytes_per_launch"] if traffic and traffic.get("workload") == wl and \
-                    fam in traffic and traffic[fam].get("bytes_per_launch") else None
+                ptr = traffic[fam]["bytes_per_launch"] if traffic and fam in traffic and \
+                    traffic[fam].get("bytes_per_launch") else None
                 out["roofline"]["pass"] = {"family": fam, "achieved": pach, "frac": pach / HBM_PEAK_GBS,
                                            "avg_launch_us": pms / pnl * 1e3, "traffic": ptr,
                                            "note": "the whole multi-way pass: k_mergek + fence merge, "

@@ -244,6 +244,12 @@ int misort_profile_read(misort_ctx* ctx, int kind, int64_t* launches, double* to
 int misort_profile_stage(misort_ctx* ctx, int stage, int64_t* count, double* exchange_ms,
                          double* merge_ms, double* exchange_bytes);
 
+/* Every profiled record since the last reset, in completion order (a
+ * multi-way pass after the k_mergek launch nested in it): kind, device ms and
+ * algorithmic bytes.  Fills up to `max` entries; returns the number recorded
+ * (at most 2^20 are kept).  For per-pass roofline figures. */
+int misort_profile_trace(misort_ctx* ctx, int max, int* kinds, double* ms, double* bytes);
+
 /* log2 of the LDS tile (keys) used for a key width of 4 or 8 bytes. */
 int misort_tile_log2(int key_bytes);
 

@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -21,6 +22,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "kernels.h"
@@ -61,6 +63,19 @@ int ilog2(int v) {
 size_t key_bytes(int dtype) { return dtype == MISORT_U32 ? 4 : 8; }
 bool valid_dtype(int dtype) { return dtype == MISORT_U32 || dtype == MISORT_U64 || dtype == MISORT_F64; }
 
+// Deadline of every wait on another rank (MISORT_TIMEOUT_S, default 120 s):
+// the role of the reference's alarm(540) watchdog (psort.cc:17,56-65), per
+// wait instead of per run, so a dead or desynchronised peer turns into an
+// error instead of a hang.
+double peer_timeout_s() {
+    static const double t = [] {
+        const char* e = getenv("MISORT_TIMEOUT_S");
+        const double v = e ? atof(e) : 120.0;
+        return v > 0 ? v : 120.0;
+    }();
+    return t;
+}
+
 // HIP-event profiler: one event pair per kernel launch of a sort.
 struct Profiler final : misort::LaunchHook {
     struct Rec {
@@ -80,6 +95,15 @@ struct Profiler final : misort::LaunchHook {
     double st_ms[MAX_STAGES][2] = {};
     double st_bytes[MAX_STAGES] = {};
     int stage = -1;
+    // every collected record in completion order (an enclosing pass after the
+    // kernels nested in it), for per-pass figures; capped
+    struct Trace {
+        int kind;
+        float ms;
+        double bytes;
+    };
+    static constexpr size_t MAX_TRACE = (size_t)1 << 20;
+    std::vector<Trace> trace;
     Rec cur{};               // the innermost open record (the exchange leg sets its bytes)
     std::vector<Rec> open;   // enclosing records (a pass around its kernel)
     bool on = false;
@@ -116,9 +140,11 @@ struct Profiler final : misort::LaunchHook {
                 HIPCHK(hipEventSynchronize(r.b));
                 HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
             }
+            if (r.kind < 0 || r.kind >= misort::KIND_COUNT) continue;
             launches[r.kind] += 1;
             ms[r.kind] += t;
             bytes[r.kind] += r.bytes;
+            if (trace.size() < MAX_TRACE) trace.push_back(Trace{r.kind, t, r.bytes});
             if (r.stage >= 0 && r.stage < MAX_STAGES) {
                 const bool xg = r.kind == misort::KIND_EXCHANGE;
                 st_ms[r.stage][xg ? 0 : 1] += t;
@@ -140,6 +166,7 @@ struct Profiler final : misort::LaunchHook {
         std::fill(std::begin(st_count), std::end(st_count), 0);
         std::fill(&st_ms[0][0], &st_ms[0][0] + 2 * MAX_STAGES, 0.0);
         std::fill(std::begin(st_bytes), std::end(st_bytes), 0.0);
+        trace.clear();
     }
     ~Profiler() override {
         for (auto& r : pending) {
@@ -180,6 +207,7 @@ struct DevBuf {
 //                   exchange is a device-to-device copy ordered by HIP events.
 struct Transport {
     int nranks = 1, rank = 0;
+    uint64_t calls = 0;  // collective calls made (entry points abort only after the first)
     virtual ~Transport() = default;
     // all ranks' int64 value, host-visible on return
     virtual int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all,
@@ -204,13 +232,184 @@ struct Transport {
     // from rank q come recv[roff[q], +rcnt[q]); every rank knows its own counts
     virtual int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv,
                           const int64_t* roff, const int64_t* rcnt, hipStream_t s) = 0;
+    // Wait for stream s, whose queue may hold transfers from other ranks,
+    // within peer_timeout_s().
+    virtual int wait(hipStream_t s) = 0;
+    // A rank failed inside a collective call: make the failure collective
+    // (the reference MPI_Abort's, psort.cc:170), so the other ranks error out
+    // instead of waiting for this one.  The transport is unusable afterwards.
+    virtual void abort_all(const char* why) = 0;
+};
+
+// Host-side watchdog for RCCL calls that can block the calling thread
+// (communicator setup, the first connection to a peer inside ncclGroupEnd):
+// armed around each such call; if the call outlives the deadline, the process
+// prints why and aborts -- the reference's SIGALRM -> program_trap -> abort()
+// (psort.cc:56-65).  Waits on the stream never block here: they poll with
+// their own deadline (RcclTransport::wait).  The thread starts on first use.
+struct CallWatchdog {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::thread th;
+    bool stop = false, armed = false;
+    const char* what = "";
+    std::chrono::steady_clock::time_point deadline;
+    void arm(const char* w) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!th.joinable()) th = std::thread([this] { loop(); });
+        what = w;
+        deadline = std::chrono::steady_clock::now() +
+                   std::chrono::microseconds((int64_t)(peer_timeout_s() * 1e6));
+        armed = true;
+        cv.notify_all();
+    }
+    void disarm() {
+        std::lock_guard<std::mutex> lk(mu);
+        armed = false;
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu);
+        while (!stop) {
+            if (!armed) {
+                cv.wait(lk);
+                continue;
+            }
+            if (cv.wait_until(lk, deadline) == std::cv_status::timeout && armed && !stop &&
+                std::chrono::steady_clock::now() >= deadline) {
+                // the blocked call holds the communicator, so it cannot be
+                // aborted safely from here: end the process (no core dump)
+                fprintf(stderr, "misort: RCCL call %s blocked for more than MISORT_TIMEOUT_S=%.0f s; exiting\n",
+                        what, peer_timeout_s());
+                fflush(stderr);
+                _exit(EXIT_FAILURE);
+            }
+        }
+    }
+    ~CallWatchdog() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        if (th.joinable()) th.join();
+    }
 };
 
 struct RcclTransport final : Transport {
     ncclComm_t comm = nullptr;
+    bool dead = false;  // aborted: every later call fails with MISORT_E_RCCL
+    std::string dead_why;
     DevBuf buf;
+    CallWatchdog dog;
     ~RcclTransport() override {
         if (comm) (void)ncclCommDestroy(comm);
+    }
+    int usable() {
+        if (dead || !comm) return fail(MISORT_E_RCCL, "RCCL communicator aborted earlier (%s)", dead_why.c_str());
+        return MISORT_OK;
+    }
+    void abort_all(const char* why) override {
+        if (dead) return;
+        dead = true;
+        dead_why = why;
+        if (comm) (void)ncclCommAbort(comm);  // peers' pending transfers fail or time out
+        comm = nullptr;
+    }
+    // An RCCL error: abort the communicator, keep the first message.
+    int rccl_fail(const char* what, ncclResult_t r) {
+        char why[512];
+        snprintf(why, sizeof why, "%s: %s", what, ncclGetErrorString(r));
+        abort_all(why);
+        return fail(MISORT_E_RCCL, "%s", why);
+    }
+    // Polls the stream and the communicator's asynchronous error state; a
+    // remote failure or the deadline aborts the communicator and returns
+    // MISORT_E_RCCL.  Spins briefly (stage waits are usually short), then
+    // sleeps between polls.
+    int wait(hipStream_t s) override {
+        int rc = usable();
+        if (rc) return rc;
+        const auto t0 = std::chrono::steady_clock::now();
+        const double lim = peer_timeout_s();
+        for (int it = 0;; ++it) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) return MISORT_OK;
+            if (q != hipErrorNotReady) {
+                abort_all("stream error while waiting for peers");
+                return fail(MISORT_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
+            }
+            ncclResult_t ar = ncclSuccess;
+            const ncclResult_t gr = ncclCommGetAsyncError(comm, &ar);
+            if (gr != ncclSuccess) return rccl_fail("ncclCommGetAsyncError", gr);
+            if (ar != ncclSuccess && ar != ncclInProgress) return rccl_fail("asynchronous RCCL error", ar);
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > lim) {
+                char why[160];
+                snprintf(why, sizeof why, "no progress from peers within MISORT_TIMEOUT_S=%.0f s", lim);
+                abort_all(why);
+                return fail(MISORT_E_RCCL, "%s", why);
+            }
+            if (it < 2000) std::this_thread::yield();
+            else std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+    }
+    // ncclGroupStart ... ncclGroupEnd that always closes the group, also when
+    // a call inside it fails, under the call watchdog.
+    template <typename F>
+    int grouped(const char* what, F&& body) {
+        ++calls;
+        int rc = usable();
+        if (rc) return rc;
+        ncclResult_t r = ncclGroupStart();
+        if (r != ncclSuccess) return rccl_fail("ncclGroupStart", r);
+        ncclResult_t inner = body();
+        dog.arm(what);
+        r = ncclGroupEnd();
+        dog.disarm();
+        if (inner != ncclSuccess) return rccl_fail(what, inner);
+        if (r != ncclSuccess) return rccl_fail(what, r);
+        return MISORT_OK;
+    }
+    // Connects every path a sort uses -- the collective ring and a send and a
+    // receive with every peer, large enough to open all of RCCL's point-to-
+    // point channels -- right after ncclCommInitRank, under the call
+    // watchdog.  RCCL connects lazily, inside ncclGroupEnd, with the peer's
+    // cooperation, so without this the first exchange with a dead or stalled
+    // peer would block the host in a call that cannot be aborted safely;
+    // afterwards a failed peer shows as a stream that does not drain, which
+    // wait() detects and aborts.
+    int connect_all(hipStream_t s) {
+        const size_t per = (size_t)8 << 20;
+        DevBuf tmp;
+        int rc = tmp.ensure(per * 2 * (size_t)nranks);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(tmp.p, 0, tmp.bytes, s));
+        char* b = (char*)tmp.p;
+        rc = grouped("connect: ncclSend/ncclRecv with every peer", [&] {
+            ncclResult_t r = ncclSuccess;
+            for (int k = 1; k < nranks && r == ncclSuccess; ++k) {
+                const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
+                r = ncclSend(b + per * to, per, ncclUint8, to, comm, s);
+                if (r == ncclSuccess) r = ncclRecv(b + per * (nranks + from), per, ncclUint8, from, comm, s);
+            }
+            return r;
+        });
+        if (rc) return rc;
+        if ((rc = buf.ensure(sizeof(int64_t) * 2 * (nranks + 1)))) return rc;
+        std::vector<int64_t> all;
+        const int64_t v[2] = {rank, nranks};
+        if ((rc = allgather_i64(v, 2, all, s))) return rc;
+        for (int r = 0; r < nranks; ++r)
+            if (all[2 * r] != r || all[2 * r + 1] != nranks) return fail(MISORT_E_RCCL, "connect: bad all-gather");
+        return wait(s);
+    }
+    int allgather_dev(const int64_t* d_src, int count, std::vector<int64_t>& all, hipStream_t s) {
+        int64_t* d = (int64_t*)buf.p;
+        int rc = grouped("ncclAllGather", [&] { return ncclAllGather(d_src, d, count, ncclInt64, comm, s); });
+        if (rc) return rc;
+        all.resize((size_t)count * nranks);
+        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
+        return wait(s);
     }
     int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
         int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
@@ -218,38 +417,31 @@ struct RcclTransport final : Transport {
         int64_t* d = (int64_t*)buf.p;
         HIPCHK(hipMemcpyAsync(d + (size_t)count * nranks, mine, sizeof(int64_t) * count,
                               hipMemcpyHostToDevice, s));
-        NCCLCHK(ncclAllGather(d + (size_t)count * nranks, d, count, ncclInt64, comm, s));
-        all.resize((size_t)count * nranks);
-        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        return MISORT_OK;
+        return allgather_dev(d + (size_t)count * nranks, count, all, s);
     }
     int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
         int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
         if (rc) return rc;
-        int64_t* d = (int64_t*)buf.p;
-        NCCLCHK(ncclAllGather(d_mine, d, count, ncclInt64, comm, s));
-        all.resize((size_t)count * nranks);
-        HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        return MISORT_OK;
+        return allgather_dev(d_mine, count, all, s);
     }
     int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
-        NCCLCHK(ncclGroupStart());
-        if (sb) NCCLCHK(ncclSend(send, sb, ncclUint8, peer, comm, s));
-        if (rb) NCCLCHK(ncclRecv(recv, rb, ncclUint8, peer, comm, s));
-        NCCLCHK(ncclGroupEnd());
-        return MISORT_OK;
+        return grouped("ncclSend/ncclRecv", [&] {
+            ncclResult_t r = ncclSuccess;
+            if (sb) r = ncclSend(send, sb, ncclUint8, peer, comm, s);
+            if (r == ncclSuccess && rb) r = ncclRecv(recv, rb, ncclUint8, peer, comm, s);
+            return r;
+        });
     }
     int group_p2p(const std::vector<Op>& ops, hipStream_t s) override {
-        NCCLCHK(ncclGroupStart());
-        for (const Op& o : ops) {
-            if (!o.bytes) continue;
-            if (o.send) NCCLCHK(ncclSend(o.sptr, o.bytes, ncclUint8, o.peer, comm, s));
-            else NCCLCHK(ncclRecv(o.rptr, o.bytes, ncclUint8, o.peer, comm, s));
-        }
-        NCCLCHK(ncclGroupEnd());
-        return MISORT_OK;
+        return grouped("grouped ncclSend/ncclRecv", [&] {
+            ncclResult_t r = ncclSuccess;
+            for (const Op& o : ops) {
+                if (!o.bytes || r != ncclSuccess) continue;
+                r = o.send ? ncclSend(o.sptr, o.bytes, ncclUint8, o.peer, comm, s)
+                           : ncclRecv(o.rptr, o.bytes, ncclUint8, o.peer, comm, s);
+            }
+            return r;
+        });
     }
     // One grouped call: every peer pair moves over its own xGMI link at once.
     int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv, const int64_t* roff,
@@ -258,14 +450,16 @@ struct RcclTransport final : Transport {
         if (scnt[rank])
             HIPCHK(hipMemcpyAsync((char*)recv + roff[rank], (const char*)send + soff[rank], (size_t)scnt[rank],
                                   hipMemcpyDeviceToDevice, s));
-        NCCLCHK(ncclGroupStart());
-        for (int k = 1; k < nranks; ++k) {
-            const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
-            if (scnt[to]) NCCLCHK(ncclSend((const char*)send + soff[to], (size_t)scnt[to], ncclUint8, to, comm, s));
-            if (rcnt[from]) NCCLCHK(ncclRecv((char*)recv + roff[from], (size_t)rcnt[from], ncclUint8, from, comm, s));
-        }
-        NCCLCHK(ncclGroupEnd());
-        return MISORT_OK;
+        return grouped("all-to-all-v ncclSend/ncclRecv", [&] {
+            ncclResult_t r = ncclSuccess;
+            for (int k = 1; k < nranks && r == ncclSuccess; ++k) {
+                const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
+                if (scnt[to]) r = ncclSend((const char*)send + soff[to], (size_t)scnt[to], ncclUint8, to, comm, s);
+                if (r == ncclSuccess && rcnt[from])
+                    r = ncclRecv((char*)recv + roff[from], (size_t)rcnt[from], ncclUint8, from, comm, s);
+            }
+            return r;
+        });
     }
 };
 
@@ -290,14 +484,24 @@ struct misort_group {
     };
     std::vector<Slot> slots;
     uint64_t bar_count = 0, bar_gen = 0;
+    bool failed = false;  // a rank failed inside a collective call: every wait ends
     explicit misort_group(int n_) : n(n_), slots(n_) {
         for (auto& sl : slots) {
             sl.posted.assign(n_, 0);
             sl.finished.assign(n_, 0);
         }
     }
+    // Waits (lock held) until pred() or a failure of the group, at most
+    // peer_timeout_s(); true iff pred() holds.
+    template <typename Pred>
+    bool wait_for(std::unique_lock<std::mutex>& lk, Pred pred) {
+        cv.wait_for(lk, std::chrono::microseconds((int64_t)(peer_timeout_s() * 1e6)),
+                    [&] { return failed || pred(); });
+        return !failed && pred();
+    }
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
         const uint64_t gen = bar_gen;
         if (++bar_count == (uint64_t)n) {
             bar_count = 0;
@@ -305,7 +509,14 @@ struct misort_group {
             cv.notify_all();
             return true;
         }
-        return cv.wait_for(lk, std::chrono::seconds(120), [&] { return bar_gen != gen; });
+        return wait_for(lk, [&] { return bar_gen != gen; });
+    }
+    void fail_all() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            failed = true;
+        }
+        cv.notify_all();
     }
 };
 
@@ -320,6 +531,11 @@ struct LocalTransport final : Transport {
         if (me.done) (void)hipEventDestroy(me.done);
         me.ready = me.done = nullptr;
     }
+    int wait(hipStream_t s) override {
+        HIPCHK(hipStreamSynchronize(s));
+        return MISORT_OK;
+    }
+    void abort_all(const char*) override { g->fail_all(); }
     int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
         std::vector<int64_t> mine((size_t)count);
         HIPCHK(hipMemcpyAsync(mine.data(), d_mine, sizeof(int64_t) * count, hipMemcpyDeviceToHost, s));
@@ -327,11 +543,12 @@ struct LocalTransport final : Transport {
         return allgather_i64(mine.data(), count, all, s);
     }
     int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t) override {
+        ++calls;
         {
             std::lock_guard<std::mutex> lk(g->mu);
             g->slots[rank].vals.assign(mine, mine + count);
         }
-        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         all.clear();
         {
             std::lock_guard<std::mutex> lk(g->mu);
@@ -339,11 +556,12 @@ struct LocalTransport final : Transport {
                 all.insert(all.end(), g->slots[r].vals.begin(), g->slots[r].vals.end());
         }
         if (!g->barrier())  // nobody overwrites vals before everyone has read them
-            return fail(MISORT_E_INVALID, "group barrier timed out");
+            return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         return MISORT_OK;
     }
     int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
         auto& me = g->slots[rank];
+        ++calls;
         auto& pe = g->slots[peer];
         const uint64_t e = ++epoch[peer];
         HIPCHK(hipEventRecord(me.ready, s));
@@ -356,8 +574,8 @@ struct LocalTransport final : Transport {
         g->cv.notify_all();
         {
             std::unique_lock<std::mutex> lk(g->mu);
-            if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return pe.posted[rank] >= e; }))
-                return fail(MISORT_E_INVALID, "group exchange %d<->%d timed out", rank, peer);
+            if (!g->wait_for(lk, [&] { return pe.posted[rank] >= e; }))
+                return fail(MISORT_E_INVALID, "group exchange %d<->%d failed or timed out", rank, peer);
         }
         if (pe.bytes != rb)
             return fail(MISORT_E_INVALID, "sendrecv size mismatch with rank %d (%zu vs %zu)", peer,
@@ -372,8 +590,8 @@ struct LocalTransport final : Transport {
         g->cv.notify_all();
         {
             std::unique_lock<std::mutex> lk(g->mu);
-            if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return pe.finished[rank] >= e; }))
-                return fail(MISORT_E_INVALID, "group exchange %d<->%d timed out", rank, peer);
+            if (!g->wait_for(lk, [&] { return pe.finished[rank] >= e; }))
+                return fail(MISORT_E_INVALID, "group exchange %d<->%d failed or timed out", rank, peer);
         }
         // the peer has read my send buffer before this stream reuses it
         HIPCHK(hipStreamWaitEvent(s, pe.done, 0));
@@ -381,6 +599,7 @@ struct LocalTransport final : Transport {
     }
     int group_p2p(const std::vector<Op>& ops, hipStream_t s) override {
         auto& me = g->slots[rank];
+        ++calls;
         HIPCHK(hipEventRecord(me.ready, s));
         {
             std::lock_guard<std::mutex> lk(g->mu);
@@ -388,7 +607,7 @@ struct LocalTransport final : Transport {
             for (const Op& o : ops)
                 if (o.send) me.p2p_send[o.peer] = {o.sptr, o.bytes};
         }
-        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         for (const Op& o : ops) {
             if (o.send) continue;
             const auto& pe = g->slots[o.peer];
@@ -400,12 +619,13 @@ struct LocalTransport final : Transport {
             HIPCHK(hipMemcpyAsync(o.rptr, pe.p2p_send[rank].first, o.bytes, hipMemcpyDeviceToDevice, s));
         }
         HIPCHK(hipStreamSynchronize(s));
-        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         return MISORT_OK;
     }
     int alltoallv(const void* send, const int64_t* soff, const int64_t* scnt, void* recv, const int64_t* roff,
                   const int64_t* rcnt, hipStream_t s) override {
         auto& me = g->slots[rank];
+        ++calls;
         HIPCHK(hipEventRecord(me.ready, s));
         {
             std::lock_guard<std::mutex> lk(g->mu);
@@ -413,7 +633,7 @@ struct LocalTransport final : Transport {
             me.a2a_off.assign(soff, soff + nranks);
             me.a2a_cnt.assign(scnt, scnt + nranks);
         }
-        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         for (int q = 0; q < nranks; ++q) {
             const auto& pe = g->slots[q];
             if (pe.a2a_cnt[rank] != rcnt[q])
@@ -426,7 +646,7 @@ struct LocalTransport final : Transport {
         }
         // every reader is done with every send buffer before anyone reuses it
         HIPCHK(hipStreamSynchronize(s));
-        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier timed out");
+        if (!g->barrier()) return fail(MISORT_E_INVALID, "group barrier failed or timed out");
         return MISORT_OK;
     }
 };
@@ -474,6 +694,28 @@ namespace {
 
 hipStream_t pick(misort_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 misort::LaunchHook* hook(misort_ctx* c) { return c->prof.on ? &c->prof : nullptr; }
+
+// Host wait on a stream whose queue may hold transfers from other ranks: with
+// a communicator, bounded by peer_timeout_s() (RCCL: polled, aborted on a
+// remote error or the deadline); a lone rank waits plainly.
+int sync(misort_ctx* c, hipStream_t s) {
+    if (c->tr) return c->tr->wait(s);
+    HIPCHK(hipStreamSynchronize(s));
+    return MISORT_OK;
+}
+
+// Result of a collective entry point: a failure after the first transport
+// call is made collective -- the communicator is aborted, so the other ranks
+// fail instead of waiting for this one (the reference MPI_Abort's,
+// psort.cc:170).  Argument errors found before any transport call stay local.
+int collective_result(misort_ctx* c, uint64_t calls0, int rc) {
+    if (rc != MISORT_OK && c->tr && c->nranks > 1 && c->tr->calls != calls0) {
+        const std::string why = g_err;
+        c->tr->abort_all(why.c_str());
+        g_err = why;
+    }
+    return rc;
+}
 
 int do_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, bool ord_in,
                   hipStream_t s, const misort::StageIO* io = nullptr) {
@@ -666,14 +908,24 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* ba
         if ((rc = c->tr->sendrecv(d_sz, 16, d_sz + 2, 16, q, s))) return rc;
         HIPCHK(hipMemcpyAsync(&all[(size_t)2 * me], d_sz, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(&all[(size_t)2 * q], d_sz + 2, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = sync(c, s))) return rc;
     }
     const int64_t raw_words = all[(size_t)2 * me + 1];
     const int64_t k = raw_words * 4 / (int64_t)w;
-    // both partners derive k from the same samples
-    if (all[(size_t)2 * q + 1] != raw_words || k < 0 || k > kmax)
-        return fail(MISORT_E_INVALID, "exchange count mismatch (%lld vs %lld words)", (long long)raw_words,
-                    (long long)all[(size_t)2 * q + 1]);
+    // Both partners derive k from the same samples.  The check is collective:
+    // a relayed stage hands every rank every pair's sizes, so every rank tests
+    // every pair and all of them fail together; at P = 2 the two partners see
+    // the same two values.
+    const int bit = ilog2(q ^ me);
+    for (int r = 0; r < c->nranks; ++r) {
+        if (!relayed && r != me) continue;
+        const int rq = r ^ (1 << bit);
+        if (all[(size_t)2 * rq + 1] != all[(size_t)2 * r + 1] || all[(size_t)2 * r + 1] < 0)
+            return fail(MISORT_E_INVALID, "exchange count mismatch between ranks %d and %d (%lld vs %lld words)", r,
+                        rq, (long long)all[(size_t)2 * r + 1], (long long)all[(size_t)2 * rq + 1]);
+    }
+    if (k < 0 || k > kmax)
+        return fail(MISORT_E_INVALID, "exchange count %lld outside [0, %lld]", (long long)k, (long long)kmax);
     *k_out = k;
     auto units = [&](int r) { return std::min(all[(size_t)2 * r], all[(size_t)2 * r + 1]); };  // 4-byte words sent
     const bool use = all[(size_t)2 * me] < raw_words;
@@ -854,13 +1106,13 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                 std::vector<uint32_t> me(cm), pe(cq);
                 HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipStreamSynchronize(s));
+                if ((rc = sync(c, s))) return rc;
                 ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
             } else {
                 std::vector<uint64_t> me(cm), pe(cq);
                 HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipStreamSynchronize(s));
+                if ((rc = sync(c, s))) return rc;
                 ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
             }
             k = na - ilo;
@@ -922,8 +1174,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
     auto key_at = [&](int64_t i, uint64_t& v) -> int {  // one key of the current run, to the host
         v = 0;
         HIPCHK(hipMemcpyAsync(&v, (const char*)c->qa.p + (size_t)i * w, w, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        return MISORT_OK;
+        return sync(c, s);
     };
     const int d = ilog2(p);
     for (int i = 0; i < d; ++i) {                       // psort.cc:389
@@ -948,7 +1199,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
         if (e != hipSuccess) return fail(MISORT_E_HIP, "lower_bound: %s", hipGetErrorString(e));
         int64_t pi = 0;                                                         // psort.cc:417
         HIPCHK(hipMemcpyAsync(&pi, dcnt, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = sync(c, s))) return rc;
         // low half keeps [0, pi) and sends [pi, rs); high half keeps [pi, rs), sends [0, pi)
         const int64_t keep_off = low ? 0 : pi, keep_n = low ? pi : rs - pi;
         const int64_t send_off = low ? pi : 0, send_n = low ? rs - pi : pi;
@@ -957,7 +1208,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
         if ((rc = c->tr->sendrecv(dcnt, 8, dcnt + 1, 8, partner, s))) return rc;
         int64_t recv_n = 0;
         HIPCHK(hipMemcpyAsync(&recv_n, dcnt + 1, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = sync(c, s))) return rc;
         if ((rc = c->recv.ensure(std::max<size_t>(16, (size_t)recv_n * w)))) return rc;
         if ((rc = c->tr->sendrecv((const char*)c->qa.p + (size_t)send_off * w, (size_t)send_n * w, c->recv.p,
                                   (size_t)recv_n * w, partner, s)))
@@ -1027,7 +1278,7 @@ int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t
         if (e != hipSuccess) return fail(MISORT_E_HIP, "gather_samples: %s", hipGetErrorString(e));
         std::vector<unsigned char> raw((size_t)cnt * w);
         HIPCHK(hipMemcpyAsync(raw.data(), c->samp_me.p, raw.size(), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = sync(c, s))) return rc;
         for (int64_t j = 0; j < cnt; ++j) {
             uint64_t v = 0;
             memcpy(&v, &raw[(size_t)j * w], w);
@@ -1075,7 +1326,7 @@ int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t
         if (e != hipSuccess) return fail(MISORT_E_HIP, "bounds: %s", hipGetErrorString(e));
         std::vector<int64_t> lbub(2 * (size_t)ns);
         HIPCHK(hipMemcpyAsync(lbub.data(), dlb, lbub.size() * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if ((rc = sync(c, s))) return rc;
         for (int j = 1; j < p; ++j) {
             const Tup& t = sp[j - 1];
             // keys of this rank below the tuple (key, rank, position) in (key, rank, position) order
@@ -1203,8 +1454,7 @@ void* misort_stream(misort_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int misort_synchronize(misort_ctx* c) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return MISORT_OK;
+    return sync(c, c->stream);
 }
 
 int misort_get_unique_id(void* id) {
@@ -1229,13 +1479,20 @@ int misort_comm_init(misort_ctx* c, int nranks, int rank, const void* id) {
         auto* t = new RcclTransport();
         ncclUniqueId u;
         memcpy(&u, id, sizeof u);
+        t->dog.arm("ncclCommInitRank");  // all ranks must join within the deadline
         ncclResult_t r = ncclCommInitRank(&t->comm, nranks, u, rank);
+        t->dog.disarm();
         if (r != ncclSuccess) {
             delete t;
             return fail(MISORT_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
         }
         t->nranks = nranks;
         t->rank = rank;
+        const int rc = t->connect_all(c->stream);
+        if (rc) {
+            delete t;
+            return rc;
+        }
         c->tr = t;
     }
     c->nranks = nranks;
@@ -1456,7 +1713,8 @@ int misort_parallel_bitonic_sort_oop(misort_ctx* c, int dtype, const void* in, v
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
     if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     if (loc > 0 && (!in || !out)) return fail(MISORT_E_INVALID, "null buffer");
-    return parallel_sort(c, dtype, in, out, loc, max_size, pick(c, stream));
+    const uint64_t calls0 = c->tr ? c->tr->calls : 0;
+    return collective_result(c, calls0, parallel_sort(c, dtype, in, out, loc, max_size, pick(c, stream)));
 }
 
 int misort_parallel_bitonic_sort(misort_ctx* c, int dtype, void* keys, int64_t loc,
@@ -1469,7 +1727,8 @@ int misort_parallel_quick_sort(misort_ctx* c, int dtype, const void* in, int64_t
     if (!c || !out_size) return fail(MISORT_E_INVALID, "null argument");
     if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     if ((loc > 0 && !in) || (out_capacity > 0 && !out)) return fail(MISORT_E_INVALID, "null buffer");
-    return parallel_quick(c, dtype, in, loc, out, out_capacity, out_size, pick(c, stream));
+    const uint64_t calls0 = c->tr ? c->tr->calls : 0;
+    return collective_result(c, calls0, parallel_quick(c, dtype, in, loc, out, out_capacity, out_size, pick(c, stream)));
 }
 
 int misort_parallel_sample_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t loc,
@@ -1478,7 +1737,8 @@ int misort_parallel_sample_sort(misort_ctx* c, int dtype, const void* in, void* 
     if (c->nranks > 1 && !c->tr) return fail(MISORT_E_NO_COMM, "communicator not initialised");
     if (loc > 0 && (!in || !out)) return fail(MISORT_E_INVALID, "null buffer");
     if (in == out && loc > 0) return fail(MISORT_E_INVALID, "sample sort is out of place (d_in != d_out)");
-    return parallel_sample(c, dtype, in, out, loc, max_size, pick(c, stream));
+    const uint64_t calls0 = c->tr ? c->tr->calls : 0;
+    return collective_result(c, calls0, parallel_sample(c, dtype, in, out, loc, max_size, pick(c, stream)));
 }
 
 int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc, const void* recv,
@@ -1526,9 +1786,12 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     }
     int64_t four[4];
     HIPCHK(hipMemcpyAsync(four, mine, sizeof four, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if ((rc = sync(c, s))) return rc;
     std::vector<int64_t> alli(four, four + 4);
-    if (p > 1 && (rc = c->tr->allgather_i64(four, 4, alli, s))) return rc;
+    if (p > 1) {
+        const uint64_t calls0 = c->tr->calls;
+        if ((rc = c->tr->allgather_i64(four, 4, alli, s))) return collective_result(c, calls0, rc);
+    }
     std::vector<uint64_t> all(alli.begin(), alli.end());
     // psort.cc:498-516: local descents + (rank>0) last(rank-1) > first(rank), SUM.
     int64_t total = 0;
@@ -1696,8 +1959,9 @@ int misort_sort_host(misort_ctx* c, int dtype, const void* h_in, void* h_out, in
         if (dtype == MISORT_F64) HIPCHK(misort::ord_to_f64((uint64_t*)(dev + k0 * w), k1 - k0, st));
         return op.push(k0, k1, st);
     };
-    if (loc == 0) return parallel_sort(c, dtype, dev, dev, 0, max_size, s);
-    if ((rc = parallel_sort(c, dtype, dev, dev, loc, max_size, s, &io))) return rc;
+    const uint64_t calls0 = c->tr ? c->tr->calls : 0;
+    if (loc == 0) return collective_result(c, calls0, parallel_sort(c, dtype, dev, dev, 0, max_size, s));
+    if ((rc = parallel_sort(c, dtype, dev, dev, loc, max_size, s, &io))) return collective_result(c, calls0, rc);
     if (!staged_out) {
         // P > 1 (or a plan whose last pass is not contiguous): chunked D2H now
         for (int i = 0; i < misort_ctx::RING; ++i)
@@ -1709,7 +1973,7 @@ int misort_sort_host(misort_ctx* c, int dtype, const void* h_in, void* h_out, in
             if ((rc = op.push(k0, std::min(loc, k0 + ch), s))) return rc;
     }
     if ((rc = op.finish())) return rc;
-    HIPCHK(hipStreamSynchronize(s));
+    if ((rc = sync(c, s))) return rc;
     return MISORT_OK;
 }
 
@@ -1755,6 +2019,19 @@ int misort_profile_stage(misort_ctx* c, int stage, int64_t* count, double* excha
     if (merge_ms) *merge_ms = c->prof.st_ms[stage][1];
     if (exchange_bytes) *exchange_bytes = c->prof.st_bytes[stage];
     return MISORT_OK;
+}
+
+int misort_profile_trace(misort_ctx* c, int max, int* kinds, double* ms, double* bytes) {
+    if (!c || max < 0 || (max > 0 && (!kinds || !ms || !bytes))) return fail(MISORT_E_INVALID, "bad trace arguments");
+    int rc = c->prof.collect();
+    if (rc) return rc;
+    const int n = (int)std::min<size_t>(c->prof.trace.size(), (size_t)max);
+    for (int i = 0; i < n; ++i) {
+        kinds[i] = c->prof.trace[i].kind;
+        ms[i] = c->prof.trace[i].ms;
+        bytes[i] = c->prof.trace[i].bytes;
+    }
+    return (int)std::min<size_t>(c->prof.trace.size(), (size_t)INT32_MAX);
 }
 
 int misort_tile_log2(int key_bytes_) { return misort::tile_log2(key_bytes_); }

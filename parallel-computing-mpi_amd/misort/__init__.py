@@ -87,6 +87,8 @@ def lib():
         "misort_profile_read": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_tile_log2": ([i32], i32),
+        "misort_profile_trace": ([vp, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double)], i32),
         "misort_profile_stage": ([vp, i32, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], i32),
         "misort_plan": ([ctypes.c_int64, i32, ctypes.POINTER(i32), i32], i32),
@@ -452,6 +454,16 @@ class Context:
                                               ctypes.byref(mm), ctypes.byref(b)))
             res.append((int(n.value), float(xm.value), float(mm.value), float(b.value)))
         return res
+
+    def profile_trace(self):
+        """[(kind_name, ms, algorithmic_bytes)] of every profiled record since the
+        last reset, in completion order (a pass after the kernel nested in it)."""
+        n = _check(lib().misort_profile_trace(self._h, 0, None, None, None))
+        k = (ctypes.c_int32 * max(n, 1))()
+        ms = (ctypes.c_double * max(n, 1))()
+        b = (ctypes.c_double * max(n, 1))()
+        _check(lib().misort_profile_trace(self._h, n, k, ms, b))
+        return [(KIND_NAMES[k[i]], ms[i], b[i]) for i in range(n)]
 
     def profile_read(self):
         """{kind: (launches, total_ms, algorithmic_bytes)}."""

@@ -33,6 +33,7 @@ root = sys.argv[1]
 # unsigned __int128 the fence merges
 U32 = not (os.environ.get("WORKLOAD") or "").startswith("u64")
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
+seq = collections.defaultdict(list)  # counter -> [(dispatch id, family, value)]
 for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
@@ -56,6 +57,9 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
         else:
             continue
         acc[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        did = r.get("Dispatch_Id") or r.get("Dispatch-Id")
+        if did is not None:
+            seq[r["Counter_Name"]].append((int(did), fam, float(r["Counter_Value"])))
 out = {"source": os.path.basename(os.path.normpath(root)),
        "workload": os.environ.get("WORKLOAD"),
        "note": "bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE correction)"}
@@ -85,5 +89,36 @@ if "run_mergek_kernel" in out:
                 m[k] = a[k] + b[k] * b["launches"] / a["launches"]
     m["note"] = "per multi-way pass: k_mergek + its planning kernels (fences, bounds, descriptors)"
     out["run_mergek"] = m
+
+# Per pass, in dispatch order (one profiled step): FETCH_SIZE and WRITE_SIZE
+# come from separate runs of the same program, matched by position.  A
+# multi-way pass is its planning kernels + k_mergek (kernel_bytes: k_mergek
+# alone); a 2-way merge level is k_runs_partition + k_runs_merge.
+def pass_list():
+    f = sorted(seq.get("FETCH_SIZE", []))
+    w = sorted(seq.get("WRITE_SIZE", []))
+    if not f or len(f) != len(w) or any(a[1] != b[1] for a, b in zip(f, w)):
+        return None
+    passes, plan, part = [], 0.0, 0.0
+    for (_, fam, fv), (_, _, wv) in zip(f, w):
+        b = fv * 1024 * (SCALE if fam.startswith("run_") else 2.0) + wv * 1024
+        if fam == "runk_plan":
+            plan += b
+        elif fam == "run_partition":
+            part += b
+        elif fam == "run_mergek_kernel":
+            passes.append({"kind": "run_mergek", "bytes": plan + b, "kernel_bytes": b})
+            plan = 0.0
+        elif fam == "run_merge_kernel":
+            passes.append({"kind": "run_merge", "bytes": part + b, "kernel_bytes": b})
+            part = 0.0
+        else:
+            passes.append({"kind": fam, "bytes": b})
+    return passes
+
+
+pl = pass_list()
+if pl:
+    out["passes"] = pl
 json.dump(out, sys.stdout, indent=1)
 print()
