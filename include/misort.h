@@ -43,7 +43,10 @@ enum misort_status {
     MISORT_E_HIP = -3,       /* HIP runtime error */
     MISORT_E_RCCL = -4,      /* RCCL error */
     MISORT_E_NO_COMM = -5,   /* communicator not initialised */
-    MISORT_E_CAPACITY = -6   /* a partner block exceeds max_size (MPI_Sendrecv truncation) */
+    MISORT_E_CAPACITY = -6,  /* a partner block exceeds max_size (MPI_Sendrecv truncation) */
+    MISORT_E_INTERNAL = -7   /* a merge pass rejected its own chunk bounds (a planning bug: the
+                                output is incomplete); reported at the next host sync of the
+                                stream (misort_synchronize, misort_check_sort) */
 };
 
 /* Kernel families reported by the per-launch profiler. */

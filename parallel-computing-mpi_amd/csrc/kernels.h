@@ -108,6 +108,8 @@ constexpr int MERGEK_FENCE_LOG2 = MISORT_MK_FG_LOG2;
 // one merge_levelk reads with that phase), for a SORT pass that writes the
 // first pass's fences itself; null on allocation failure.
 void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s);
+void mergek_release(hipStream_t s);
+int mergek_take_error(hipStream_t s);
 int merge_levelk_lw_min(int key_bytes);   // shortest input runs (log2) of a multi-way pass
 int merge_levelk_lwk_max(int key_bytes);  // largest output runs (log2)
 

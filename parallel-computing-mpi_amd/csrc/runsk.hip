@@ -602,7 +602,7 @@ struct DescHdr {
 
 template <typename KEY, int LK, int DC>
 __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo, int64_t nchunks,
-                                                   Desc<KEY, LK>* __restrict__ desc) {
+                                                   Desc<KEY, LK>* __restrict__ desc, int* __restrict__ err) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NROWS = S::NROWS;
     __shared__ DescHdr<KEY, LK> hdr[DC];
@@ -630,6 +630,7 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
             tot += ln;
         }
         ok = ok && tot <= S::CAP;
+        if (!ok) atomicOr(err, 1);  // a planning bug: the chunk stays unwritten, the host is told
         DescHdr<KEY, LK>& h = hdr[lane];
         int R = 0, o = 0;
         int64_t out = geo.base(g);
@@ -923,6 +924,24 @@ void* scratch(int which, size_t bytes, hipStream_t s) {
     return e.p;
 }
 
+// One error word per (device, stream): k_chunk_desc sets it when it rejects
+// a chunk's bounds (mergek_take_error reads and clears it).
+std::map<std::pair<int, hipStream_t>, int*> g_errw;
+int* error_word(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_mu);
+    int*& w = g_errw[{dev, s}];
+    if (!w) {
+        if (hipMalloc(&w, sizeof(int)) != hipSuccess) {
+            w = nullptr;
+            return nullptr;
+        }
+        if (hipMemsetAsync(w, 0, sizeof(int), s) != hipSuccess) return nullptr;
+    }
+    return w;
+}
+
 int64_t chunks_of(const Geo& geo) {
     const bool tail = (geo.nfull << (geo.lw + geo.lk)) < geo.n;
     return geo.nfull * geo.kf + (tail ? geo.nchunks(geo.nfull) : 0);
@@ -952,7 +971,8 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
     char* fbase = (char*)scratch(0, 2 * fb, s);
     char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
-    if (!base || !fbase) return hipErrorOutOfMemory;
+    int* ew = error_word(s);
+    if (!base || !fbase || !ew) return hipErrorOutOfMemory;
     FT* F = (FT*)(fbase + (phase & 1) * fb);
     FT* Fn = (FT*)(fbase + ((phase & 1) ^ 1) * fb);
     FT* M = (FT*)base;
@@ -999,8 +1019,8 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
     k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo, nslots,
                                                                           bounds, (nslots << LK) >= line_min);
-    if (nchunks >= dc16_min) k_chunk_desc<KEY, LK, 16><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
-    else k_chunk_desc<KEY, LK, 4><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks, desc);
+    if (nchunks >= dc16_min) k_chunk_desc<KEY, LK, 16><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks, desc, ew);
+    else k_chunk_desc<KEY, LK, 4><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks, desc, ew);
     const unsigned grid = (unsigned)nchunks;
     if (hook) hook->before(KIND_RUNSK_KERNEL, 2.0 * (double)n * sizeof(KEY), s);
     if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
@@ -1062,6 +1082,48 @@ void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
     const size_t fb = ((size_t)nf * (key_bytes == 8 ? sizeof(u128) : sizeof(uint64_t)) + 255) & ~(size_t)255;
     char* fbase = (char*)scratch(0, 2 * fb, s);
     return fbase ? fbase + (phase & 1) * fb : nullptr;
+}
+// 1 if a merge pass on stream s rejected a chunk since the last call (the
+// stream is synchronised), else 0; negative on a HIP error.
+int mergek_take_error(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    int* w = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_errw.find({dev, s});
+        if (it == g_errw.end()) return 0;
+        w = it->second;
+    }
+    int v = 0;
+    if (hipMemcpyAsync(&v, w, sizeof v, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    if (v && (hipMemsetAsync(w, 0, sizeof(int), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) return -1;
+    return v ? 1 : 0;
+}
+
+// Frees the fence and planning scratch kept for stream s on the current
+// device (misort_destroy, for the context's own stream).
+void mergek_release(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto ew = g_errw.find({dev, s});
+    if (ew != g_errw.end()) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(ew->second);
+        g_errw.erase(ew);
+    }
+    for (auto& m : g_scr) {
+        auto it = m.find({dev, s});
+        if (it == m.end()) continue;
+        if (it->second.p) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(it->second.p);
+        }
+        m.erase(it);
+    }
 }
 int merge_levelk_lw_min(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LW_MIN : KTr<uint32_t>::LW_MIN; }
 int merge_levelk_lwk_max(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LWK_MAX : KTr<uint32_t>::LWK_MAX; }

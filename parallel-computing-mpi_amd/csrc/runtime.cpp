@@ -104,7 +104,7 @@ struct Profiler final : misort::LaunchHook {
     };
     static constexpr size_t MAX_TRACE = (size_t)1 << 20;
     std::vector<Trace> trace;
-    Rec cur{};               // the innermost open record (the exchange leg sets its bytes)
+    Rec cur{-1, nullptr, nullptr, 0.0, -1};             // the innermost open record (the exchange leg sets its bytes)
     std::vector<Rec> open;   // enclosing records (a pass around its kernel)
     bool on = false;
 
@@ -119,7 +119,7 @@ struct Profiler final : misort::LaunchHook {
         return e;
     }
     void before(misort::Kind k, double b, hipStream_t s) override {
-        if (cur.kind >= 0 && (cur.a || cur.b)) open.push_back(cur);
+        if (cur.kind >= 0) open.push_back(cur);
         cur = Rec{k, take(), take(), b, stage};
         if (cur.a) (void)hipEventRecord(cur.a, s);
     }
@@ -704,6 +704,15 @@ int sync(misort_ctx* c, hipStream_t s) {
     return MISORT_OK;
 }
 
+// The merge passes' device error word of stream s (k_chunk_desc rejected a
+// chunk): the stream is synchronised.
+int planning_check(hipStream_t s) {
+    const int e = misort::mergek_take_error(s);
+    if (e < 0) return fail(MISORT_E_HIP, "reading the merge passes' error word failed");
+    if (e > 0) return fail(MISORT_E_INTERNAL, "a merge pass rejected its chunk bounds: the sorted output is incomplete");
+    return MISORT_OK;
+}
+
 // Result of a collective entry point: a failure after the first transport
 // call is made collective -- the communicator is aborted, so the other ranks
 // fail instead of waiting for this one (the reference MPI_Abort's,
@@ -1040,15 +1049,25 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
     };
     for (int st = 0; st < nst; ++st) {
         StageMark mark(c->prof, st);
-        if (hk) hk->before(misort::KIND_EXCHANGE, 0.0, s);
-        bool xg_open = hk != nullptr;
-        auto xg_close = [&](double bytes) {
-            if (xg_open) {
-                c->prof.cur.bytes = bytes;
-                hk->after(misort::KIND_EXCHANGE, s);
-                xg_open = false;
+        // the exchange leg's profiler record, closed on every way out of the
+        // stage (error returns included) so later records never nest in it
+        struct XgRecord {
+            misort::LaunchHook* hk;
+            Profiler& pr;
+            hipStream_t s;
+            bool open;
+            XgRecord(misort::LaunchHook* h, Profiler& p_, hipStream_t s_) : hk(h), pr(p_), s(s_), open(h != nullptr) {
+                if (hk) hk->before(misort::KIND_EXCHANGE, 0.0, s);
             }
-        };
+            void close(double bytes) {
+                if (!open) return;
+                pr.cur.bytes = bytes;
+                hk->after(misort::KIND_EXCHANGE, s);
+                open = false;
+            }
+            ~XgRecord() { close(0.0); }
+        } xg(hk, c->prof, s);
+        auto xg_close = [&](double bytes) { xg.close(bytes); };
         const int q = partner[st];
         const int64_t nq = sizes[q];
         const bool mx = keep[st] != 0;  // this rank keeps the upper part
@@ -1445,7 +1464,10 @@ int misort_destroy(misort_ctx* c) {
     delete c->tr;
     c->tr = nullptr;
     if (c->pinned) (void)hipHostFree(c->pinned);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream) {
+        misort::mergek_release(c->stream);  // the merge passes' scratch for this stream
+        (void)hipStreamDestroy(c->stream);
+    }
     delete c;
     return MISORT_OK;
 }
@@ -1454,7 +1476,8 @@ void* misort_stream(misort_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int misort_synchronize(misort_ctx* c) {
     if (!c) return fail(MISORT_E_INVALID, "null ctx");
-    return sync(c, c->stream);
+    int rc = sync(c, c->stream);
+    return rc ? rc : planning_check(c->stream);
 }
 
 int misort_get_unique_id(void* id) {
@@ -1784,15 +1807,24 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
         HIPCHK(hipMemcpyAsync(mine + 2, keys, w, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(mine + 3, (const char*)keys + (size_t)(n - 1) * w, w, hipMemcpyDeviceToDevice, s));
     }
-    int64_t four[4];
-    HIPCHK(hipMemcpyAsync(four, mine, sizeof four, hipMemcpyDeviceToHost, s));
+    // ... and a fifth word: this rank's merge passes rejected a chunk (gathered
+    // with the rest, so every rank reports it together)
+    int64_t four[5];
+    HIPCHK(hipMemcpyAsync(four, mine, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     if ((rc = sync(c, s))) return rc;
-    std::vector<int64_t> alli(four, four + 4);
+    const int perr = planning_check(s);
+    if (perr == MISORT_E_HIP) return perr;
+    four[4] = perr != MISORT_OK;
+    std::vector<int64_t> alli(four, four + 5);
     if (p > 1) {
         const uint64_t calls0 = c->tr->calls;
-        if ((rc = c->tr->allgather_i64(four, 4, alli, s))) return collective_result(c, calls0, rc);
+        if ((rc = c->tr->allgather_i64(four, 5, alli, s))) return collective_result(c, calls0, rc);
     }
-    std::vector<uint64_t> all(alli.begin(), alli.end());
+    for (int r = 0; r < p; ++r)
+        if (alli[5 * (size_t)r + 4])
+            return fail(MISORT_E_INTERNAL, "rank %d: a merge pass rejected its chunk bounds (incomplete output)", r);
+    std::vector<uint64_t> all;
+    for (int r = 0; r < p; ++r) all.insert(all.end(), alli.begin() + 5 * (size_t)r, alli.begin() + 5 * (size_t)r + 4);
     // psort.cc:498-516: local descents + (rank>0) last(rank-1) > first(rank), SUM.
     int64_t total = 0;
     bool have_prev = false;

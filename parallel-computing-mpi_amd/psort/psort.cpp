@@ -153,9 +153,16 @@ int main(int argc, char** argv) {
     long long input_size = 1024;  // psort.cc:538
     std::string keys_file, out_file, dtype_s = "f64";
     bool verbose = false;
-    // psort.cc:541-544 takes argv[1] as N; here the one positional argument is N
-    // wherever it stands, so extension flags never read as the key count.
-    for (int a = 1; a < argc; ++a) {
+    // psort.cc:541-544 reads N from argv[1] when argc == 2 and ignores every
+    // other argument.  Without extension flags this driver does the same; with
+    // them (each starts with "--"), the one positional argument is N wherever
+    // it stands, and an unknown "--" option is an error.
+    bool ext = false;
+    for (int a = 1; a < argc; ++a) ext = ext || (argv[a][0] == '-' && argv[a][1] == '-');
+    if (!ext) {
+        if (argc == 2) input_size = atoll(argv[1]);
+    }
+    for (int a = 1; ext && a < argc; ++a) {
         std::string s = argv[a];
         auto value = [&]() -> std::string {
             if (a + 1 >= argc) {
@@ -206,20 +213,29 @@ int main(int argc, char** argv) {
     if (myid < remainder) local_input_size += 1;
     const long long offset = (input_size / numprocs) * myid + (myid < remainder ? myid : remainder);
 
-    // One GPU per rank; RCCL communicator in place of MPI_COMM_WORLD.
+    // One GPU per rank; RCCL communicator in place of MPI_COMM_WORLD.  GPUs
+    // are assigned by the rank's place among the ranks of ITS node (a job may
+    // span nodes: the reference's PBS runs use 7 nodes x 20 cores).
     int ndev = 0;
     HIP_OK(hipGetDeviceCount(&ndev));
+    MPI_Comm node;
+    MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, myid, MPI_INFO_NULL, &node);
+    int local_rank = 0, local_size = 1;
+    MPI_Comm_rank(node, &local_rank);
+    MPI_Comm_size(node, &local_size);
+    MPI_Comm_free(&node);
     const char* dev_env = getenv("PSORT_DEVICE");
-    const int dev = dev_env ? atoi(dev_env) : myid % std::max(1, ndev);
-    if (numprocs > std::max(1, ndev) && !dev_env) {
-        // GPUs shared by ranks: one host id per rank, RCCL over loopback sockets
+    const int dev = dev_env ? atoi(dev_env) : local_rank % std::max(1, ndev);
+    if (local_size > std::max(1, ndev) && !dev_env) {
+        // more ranks than GPUs on this node: one host id per rank, RCCL over
+        // loopback sockets (a correctness mode, single node only)
         char hid[64];
         snprintf(hid, sizeof hid, "psort-shared-gpu-rank%d", myid);
         setenv("NCCL_HOSTID", hid, 1);
         setenv("NCCL_SOCKET_IFNAME", "lo", 0);
         if (myid == 0 && verbose)
-            fprintf(stderr, "psort: %d ranks on %d GPU(s): RCCL over sockets (correctness mode)\n", numprocs,
-                    ndev);
+            fprintf(stderr, "psort: %d ranks on %d GPU(s) of a node: RCCL over sockets (correctness mode)\n",
+                    local_size, ndev);
     }
     // RCCL logs (its version banner included) go to NCCL_DEBUG_FILE, stdout by
     // default: keep stdout the reference's six lines
