@@ -25,12 +25,14 @@ rate of every hypercube stage, and t1 / (P * tP) against a 1-GPU leg of the
 same keys run in the same job.
 """
 import argparse
+import faulthandler
 import json
 import os
 import re
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -63,6 +65,10 @@ def parse_args(argv=None):
                          "workload (BASELINE.md section 3), reported under cpu_sweep")
     ap.add_argument("--cpu-sweep-logn", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--watchdog-s", type=float, default=1200.0,
+                    help="a rank still running after this many seconds prints every thread's stack and "
+                         "exits (1): a hang ends as an error, as the reference's alarm(540) does "
+                         "(psort.cc:17,56-65); each wait on a peer is bounded by MISORT_TIMEOUT_S too")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time without per-launch HIP events (roofline omitted)")
     ap.add_argument("--host-io", action="store_true",
@@ -214,6 +220,20 @@ def port_baseline(logn, why):
             "fallback_reason": why}
 
 
+CPU_JSON_ENV = "MISORT_BENCH_CPU_JSON"
+
+
+def load_cpu_json(path):
+    """The host-core baseline the launcher parent measured (or None)."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        cpu = json.load(f)
+    if isinstance(cpu, dict):
+        cpu["measured_by"] = "bench.py launcher parent, before the GPU ranks started"
+    return cpu
+
+
 def load_traffic(workload):
     """Per-launch HBM bytes of this exact workload from the committed rocprofv3
     --pmc summary profiles/traffic_<workload>.json (tools/traffic.py), or None
@@ -293,22 +313,43 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
     if needs_launch(args):
-        # one process per GPU; this process never touches the GPU
+        # one process per GPU; this process never touches the GPU.  It runs the
+        # host-core baseline first (the reference under mpirun on this host's
+        # cores) and hands it to rank 0 in a file, so the N-GPU line carries it.
         cmd = launch_command(argv, args.gpus, free_port())
-        return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        path = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
+                               args.cpu_sweep, args.cpu_sweep_logn)
+            fd, path = tempfile.mkstemp(prefix="misort_bench_cpu_", suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(cpu, f)
+            env[CPU_JSON_ENV] = path
+        try:
+            return subprocess.call(cmd, env=env)
+        finally:
+            if path:
+                os.remove(path)
 
+    if args.watchdog_s > 0:
+        faulthandler.dump_traceback_later(args.watchdog_s, exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.gpus != world:
         sys.stderr.write(f"WARNING --gpus {args.gpus} but WORLD_SIZE {world}: running {world} ranks\n")
 
-    # The CPU baseline runs first, before this process touches the GPU
-    # (rank 0 at N = 1 only).
+    # The CPU baseline runs first, before this process touches the GPU, on
+    # rank 0 at every N (the other ranks wait in the process-group setup):
+    # the reference's parallel_bitonic_sort under mpirun on the host cores,
+    # or the launcher parent's measurement of it when there was one.
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
-                           args.cpu_sweep, args.cpu_sweep_logn)
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = load_cpu_json(os.environ.get(CPU_JSON_ENV))
+        if cpu is None:
+            cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
+                               args.cpu_sweep, args.cpu_sweep_logn)
 
     # RCCL logs (its version banner too) go to stderr: stdout is the JSON line
     os.environ.setdefault("NCCL_DEBUG_FILE", "/dev/stderr")

@@ -45,6 +45,7 @@ def test_main_relaunches_without_touching_the_gpu(monkeypatch):
 
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(b.subprocess, "call", fake_call)
+    monkeypatch.setattr(b, "cpu_baseline", lambda *a: {"value": 0.1, "kind": "reference", "cores": 16})
     # if main went past the launcher it would build contexts: make that fatal
     import misort
     monkeypatch.setattr(misort, "Context", lambda *a, **k: (_ for _ in ()).throw(AssertionError("GPU touched")))
@@ -54,6 +55,30 @@ def test_main_relaunches_without_touching_the_gpu(monkeypatch):
     assert "--nproc-per-node=8" in cmd
     assert cmd[-4:] == ["--gpus", "8", "--steps", "2"]
     assert env["MASTER_ADDR"] == "127.0.0.1"
+    # the host-core baseline was measured by the parent and handed over
+    # (the file is removed once the ranks have finished)
+    assert b.CPU_JSON_ENV in env and not os.path.exists(env[b.CPU_JSON_ENV])
+
+
+def test_parent_cpu_baseline_reaches_rank0(monkeypatch, tmp_path):
+    """The N > 1 line carries the host-core baseline: the parent measures it
+    (no HIP call: misort.Context is fatal here) and rank 0 loads it."""
+    b = load_bench()
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cpu"] = b.load_cpu_json(env[b.CPU_JSON_ENV])
+        return 0
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(b.subprocess, "call", fake_call)
+    monkeypatch.setattr(b, "cpu_baseline", lambda *a: {"value": 0.12, "kind": "reference", "cores": 16})
+    import misort
+    monkeypatch.setattr(misort, "Context", lambda *a, **k: (_ for _ in ()).throw(AssertionError("GPU touched")))
+    assert b.main(["--gpus", "4"]) == 0
+    assert seen["cpu"]["value"] == 0.12 and seen["cpu"]["kind"] == "reference"
+    assert "launcher parent" in seen["cpu"]["measured_by"]
+    assert b.load_cpu_json(None) is None and b.load_cpu_json(str(tmp_path / "missing.json")) is None
 
 
 def test_cpu_share_and_pow2():
