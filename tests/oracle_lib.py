@@ -24,7 +24,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        path = os.path.join(ORACLE_DIR, "liboracle.so")
+        path = os.environ.get("ORACLE_LIBRARY") or os.path.join(ORACLE_DIR, "liboracle.so")
         if not os.path.exists(path):
             subprocess.run(["make", "-s", "-C", ORACLE_DIR, "oracle"], check=True)
         L = ctypes.CDLL(path)
