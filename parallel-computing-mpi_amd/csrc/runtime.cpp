@@ -19,6 +19,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <new>
 #include <string>
 #include <thread>
@@ -30,6 +31,21 @@
 namespace {
 
 thread_local std::string g_err;
+
+// MISORT_TRACE=1: one stderr line per RCCL-side step (group calls, waits,
+// aborts), to see where a multi-rank run stands when it stops.
+bool trace_on() {
+    static const bool on = getenv("MISORT_TRACE") && atoi(getenv("MISORT_TRACE")) != 0;
+    return on;
+}
+#define TRACE(...)                                  \
+    do {                                            \
+        if (trace_on()) {                           \
+            fprintf(stderr, "[misort] " __VA_ARGS__); \
+            fputc('\n', stderr);                    \
+            fflush(stderr);                         \
+        }                                           \
+    } while (0)
 
 int fail(int code, const char* fmt, ...) {
     char buf[1024];
@@ -312,7 +328,9 @@ struct RcclTransport final : Transport {
         if (dead) return;
         dead = true;
         dead_why = why;
+        TRACE("rank %d: aborting the communicator (%s)", rank, why);
         if (comm) (void)ncclCommAbort(comm);  // peers' pending transfers fail or time out
+        TRACE("rank %d: communicator aborted", rank);
         comm = nullptr;
     }
     // An RCCL error: abort the communicator, keep the first message.
@@ -329,6 +347,7 @@ struct RcclTransport final : Transport {
     int wait(hipStream_t s) override {
         int rc = usable();
         if (rc) return rc;
+        TRACE("rank %d: waiting on the stream (deadline %.0f s)", rank, peer_timeout_s());
         const auto t0 = std::chrono::steady_clock::now();
         const double lim = peer_timeout_s();
         for (int it = 0;; ++it) {
@@ -363,9 +382,11 @@ struct RcclTransport final : Transport {
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess) return rccl_fail("ncclGroupStart", r);
         ncclResult_t inner = body();
+        TRACE("rank %d: ncclGroupEnd (%s)", rank, what);
         dog.arm(what);
         r = ncclGroupEnd();
         dog.disarm();
+        TRACE("rank %d: ncclGroupEnd returned %d", rank, (int)r);
         if (inner != ncclSuccess) return rccl_fail(what, inner);
         if (r != ncclSuccess) return rccl_fail(what, r);
         return MISORT_OK;
@@ -407,21 +428,25 @@ struct RcclTransport final : Transport {
         int64_t* d = (int64_t*)buf.p;
         int rc = grouped("ncclAllGather", [&] { return ncclAllGather(d_src, d, count, ncclInt64, comm, s); });
         if (rc) return rc;
+        // drain the stream under the deadline first: a device-to-host copy
+        // into pageable memory would block on it without one
+        if ((rc = wait(s))) return rc;
         all.resize((size_t)count * nranks);
         HIPCHK(hipMemcpyAsync(all.data(), d, sizeof(int64_t) * count * nranks, hipMemcpyDeviceToHost, s));
-        return wait(s);
+        HIPCHK(hipStreamSynchronize(s));
+        return MISORT_OK;
     }
     int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
-        int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
-        if (rc) return rc;
+        int rc = usable();
+        if (rc || (rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1)))) return rc;
         int64_t* d = (int64_t*)buf.p;
         HIPCHK(hipMemcpyAsync(d + (size_t)count * nranks, mine, sizeof(int64_t) * count,
                               hipMemcpyHostToDevice, s));
         return allgather_dev(d + (size_t)count * nranks, count, all, s);
     }
     int allgather_i64_dev(const int64_t* d_mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
-        int rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1));
-        if (rc) return rc;
+        int rc = usable();
+        if (rc || (rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1)))) return rc;
         return allgather_dev(d_mine, count, all, s);
     }
     int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
@@ -704,6 +729,22 @@ int sync(misort_ctx* c, hipStream_t s) {
     return MISORT_OK;
 }
 
+// Small device -> host copies after work that may include transfers from
+// other ranks: the stream is drained first by the bounded wait (a copy into
+// pageable memory would block on an undrained stream with no deadline).
+struct D2H {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+int fetch(misort_ctx* c, hipStream_t s, std::initializer_list<D2H> cps) {
+    int rc = sync(c, s);
+    if (rc) return rc;
+    for (const D2H& x : cps) HIPCHK(hipMemcpyAsync(x.dst, x.src, x.bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return MISORT_OK;
+}
+
 // The merge passes' device error word of stream s (k_chunk_desc rejected a
 // chunk): the stream is synchronised.
 int planning_check(hipStream_t s) {
@@ -915,9 +956,7 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* ba
         // P = 2 (or no relay): the partner's pair by sendrecv, mine by copy
         all.assign((size_t)2 * c->nranks, 0);
         if ((rc = c->tr->sendrecv(d_sz, 16, d_sz + 2, 16, q, s))) return rc;
-        HIPCHK(hipMemcpyAsync(&all[(size_t)2 * me], d_sz, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(&all[(size_t)2 * q], d_sz + 2, 16, hipMemcpyDeviceToHost, s));
-        if ((rc = sync(c, s))) return rc;
+        if ((rc = fetch(c, s, {{&all[(size_t)2 * me], d_sz, 16}, {&all[(size_t)2 * q], d_sz + 2, 16}}))) return rc;
     }
     const int64_t raw_words = all[(size_t)2 * me + 1];
     const int64_t k = raw_words * 4 / (int64_t)w;
@@ -1123,15 +1162,13 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             int64_t ilo;
             if (w == 4) {
                 std::vector<uint32_t> me(cm), pe(cq);
-                HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
-                if ((rc = sync(c, s))) return rc;
+                if ((rc = fetch(c, s, {{me.data(), c->samp_me.p, cm * w}, {pe.data(), c->samp_peer.p, cq * w}})))
+                    return rc;
                 ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
             } else {
                 std::vector<uint64_t> me(cm), pe(cq);
-                HIPCHK(hipMemcpyAsync(me.data(), c->samp_me.p, cm * w, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(pe.data(), c->samp_peer.p, cq * w, hipMemcpyDeviceToHost, s));
-                if ((rc = sync(c, s))) return rc;
+                if ((rc = fetch(c, s, {{me.data(), c->samp_me.p, cm * w}, {pe.data(), c->samp_peer.p, cq * w}})))
+                    return rc;
                 ilo = mx ? corank_lower(pe, na, me, nb) : corank_lower(me, na, pe, nb);
             }
             k = na - ilo;
@@ -1192,8 +1229,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
     uint64_t stale0 = 0;  // result_buffer[0] as last written: the median of an empty rank (psort.cc:399)
     auto key_at = [&](int64_t i, uint64_t& v) -> int {  // one key of the current run, to the host
         v = 0;
-        HIPCHK(hipMemcpyAsync(&v, (const char*)c->qa.p + (size_t)i * w, w, hipMemcpyDeviceToHost, s));
-        return sync(c, s);
+        return fetch(c, s, {{&v, (const char*)c->qa.p + (size_t)i * w, w}});
     };
     const int d = ilog2(p);
     for (int i = 0; i < d; ++i) {                       // psort.cc:389
@@ -1217,8 +1253,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
                               : misort::lower_bound<uint64_t>((const uint64_t*)c->qa.p, rs, pivot, dcnt, s);
         if (e != hipSuccess) return fail(MISORT_E_HIP, "lower_bound: %s", hipGetErrorString(e));
         int64_t pi = 0;                                                         // psort.cc:417
-        HIPCHK(hipMemcpyAsync(&pi, dcnt, 8, hipMemcpyDeviceToHost, s));
-        if ((rc = sync(c, s))) return rc;
+        if ((rc = fetch(c, s, {{&pi, dcnt, 8}}))) return rc;
         // low half keeps [0, pi) and sends [pi, rs); high half keeps [pi, rs), sends [0, pi)
         const int64_t keep_off = low ? 0 : pi, keep_n = low ? pi : rs - pi;
         const int64_t send_off = low ? pi : 0, send_n = low ? rs - pi : pi;
@@ -1226,8 +1261,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
         HIPCHK(hipMemcpyAsync(dcnt, &send_n, 8, hipMemcpyHostToDevice, s));
         if ((rc = c->tr->sendrecv(dcnt, 8, dcnt + 1, 8, partner, s))) return rc;
         int64_t recv_n = 0;
-        HIPCHK(hipMemcpyAsync(&recv_n, dcnt + 1, 8, hipMemcpyDeviceToHost, s));
-        if ((rc = sync(c, s))) return rc;
+        if ((rc = fetch(c, s, {{&recv_n, dcnt + 1, 8}}))) return rc;
         if ((rc = c->recv.ensure(std::max<size_t>(16, (size_t)recv_n * w)))) return rc;
         if ((rc = c->tr->sendrecv((const char*)c->qa.p + (size_t)send_off * w, (size_t)send_n * w, c->recv.p,
                                   (size_t)recv_n * w, partner, s)))
@@ -1296,8 +1330,7 @@ int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t
                                                                  (uint64_t*)c->samp_me.p, cnt, s);
         if (e != hipSuccess) return fail(MISORT_E_HIP, "gather_samples: %s", hipGetErrorString(e));
         std::vector<unsigned char> raw((size_t)cnt * w);
-        HIPCHK(hipMemcpyAsync(raw.data(), c->samp_me.p, raw.size(), hipMemcpyDeviceToHost, s));
-        if ((rc = sync(c, s))) return rc;
+        if ((rc = fetch(c, s, {{raw.data(), c->samp_me.p, raw.size()}}))) return rc;
         for (int64_t j = 0; j < cnt; ++j) {
             uint64_t v = 0;
             memcpy(&v, &raw[(size_t)j * w], w);
@@ -1344,8 +1377,7 @@ int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t
                                                          ns, dlb, dub, s);
         if (e != hipSuccess) return fail(MISORT_E_HIP, "bounds: %s", hipGetErrorString(e));
         std::vector<int64_t> lbub(2 * (size_t)ns);
-        HIPCHK(hipMemcpyAsync(lbub.data(), dlb, lbub.size() * 8, hipMemcpyDeviceToHost, s));
-        if ((rc = sync(c, s))) return rc;
+        if ((rc = fetch(c, s, {{lbub.data(), dlb, lbub.size() * 8}}))) return rc;
         for (int j = 1; j < p; ++j) {
             const Tup& t = sp[j - 1];
             // keys of this rank below the tuple (key, rank, position) in (key, rank, position) order
@@ -1810,8 +1842,7 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     // ... and a fifth word: this rank's merge passes rejected a chunk (gathered
     // with the rest, so every rank reports it together)
     int64_t four[5];
-    HIPCHK(hipMemcpyAsync(four, mine, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    if ((rc = sync(c, s))) return rc;
+    if ((rc = fetch(c, s, {{four, mine, 4 * sizeof(int64_t)}}))) return rc;
     const int perr = planning_check(s);
     if (perr == MISORT_E_HIP) return perr;
     four[4] = perr != MISORT_OK;

@@ -71,6 +71,8 @@ def main():
         sys.stderr.flush()
 
     if mode in ("stall", "dead"):
+        import faulthandler
+        faulthandler.dump_traceback_later(90, exit=True)  # a hang shows where, then ends
         dist.barrier()
         log("communicator up, peer " + ("leaves" if mode == "dead" else "stalls"))
         if rank == 1:

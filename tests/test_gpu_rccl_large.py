@@ -97,7 +97,7 @@ def test_rccl_baseline_size(p, args):
 @pytest.mark.parametrize("mode", ["stall", "dead"])
 def test_rccl_failed_peer_errors_instead_of_hanging(mode):
     limit = 15
-    rc, res = launch(2, [mode], timeout=120, extra_env={"MISORT_TIMEOUT_S": str(limit),
+    rc, res = launch(2, [mode], timeout=120, extra_env={"MISORT_TIMEOUT_S": str(limit), "MISORT_TRACE": "1",
                                                        "MISORT_TEST_STALL_S": str(limit + 25)})
     assert res["mode"] == mode
     assert res["code"] == MISORT_E_RCCL, res
