@@ -932,7 +932,8 @@ int relay_raw(misort_ctx* c, int bit, const void* sbuf, size_t bytes, void* rbuf
 // this rank); *rkeys receives the partner's k keys (decoded into c->recv, or
 // the raw message in c->enc_recv when the partner sent it uncoded).
 int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* base, int64_t nloc, bool keep_max,
-                   const int64_t* run, int64_t kmax, int64_t* k_out, const void** rkeys, hipStream_t s) {
+                   const int64_t* run, int64_t kmax, int64_t* k_out, const void** rkeys, hipStream_t s,
+                   const std::function<bool(int, int)>& pair_coded) {
     const size_t w = key_bytes(dtype);
     const int64_t maxw = misort::codec_max_words(kmax, (int)w), raw_max = kmax * (int64_t)w / 4;
     int rc;
@@ -968,6 +969,9 @@ int coded_exchange(misort_ctx* c, int dtype, int q, bool relayed, const void* ba
     for (int r = 0; r < c->nranks; ++r) {
         if (!relayed && r != me) continue;
         const int rq = r ^ (1 << bit);
+        // pairs with an empty block exchange whole blocks raw in the same
+        // relayed stage (relay_raw): their sizes legitimately differ
+        if (r != me && !pair_coded(r, rq)) continue;
         if (all[(size_t)2 * rq + 1] != all[(size_t)2 * r + 1] || all[(size_t)2 * r + 1] < 0)
             return fail(MISORT_E_INVALID, "exchange count mismatch between ranks %d and %d (%lld vs %lld words)", r,
                         rq, (long long)all[(size_t)2 * r + 1], (long long)all[(size_t)2 * rq + 1]);
@@ -1121,8 +1125,12 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         // the codec's offsets and word totals are 32-bit: messages that could
         // reach 2^32 words go raw (both sides decide from the same bound)
         const int64_t kmax = std::min(na, nb);
-        const bool coded = !c->full_exchange && loc > 0 && nq > 0 && c->compress &&
-                           misort::codec_max_words(kmax, (int)w) < ((int64_t)1 << 32);
+        // the same rule for every pair of the stage (every rank knows every block size)
+        auto pair_coded = [&](int r, int rq) {
+            const int64_t km = std::min(sizes[r], sizes[rq]);
+            return !c->full_exchange && km > 0 && c->compress && misort::codec_max_words(km, (int)w) < ((int64_t)1 << 32);
+        };
+        const bool coded = pair_coded(c->rank, q);
         if (!c->full_exchange && loc > 0 && nq > 0) {
             const int64_t cm = sample_count(loc), cq = sample_count(nq);
             hipError_t e = w == 4 ? misort::gather_samples<uint32_t>((const uint32_t*)cur, loc, sample_stride(loc),
@@ -1144,7 +1152,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                                   : misort::exchange_count<uint64_t>((const uint64_t*)sa, na, (const uint64_t*)sb,
                                                                      nb, mx, loc, d_run, s);
             if (e != hipSuccess) return fail(MISORT_E_HIP, "exchange_count: %s", hipGetErrorString(e));
-            if ((rc = coded_exchange(c, dtype, q, relayed, cur, loc, mx, d_run, kmax, &k, &rkeys, s))) return rc;
+            if ((rc = coded_exchange(c, dtype, q, relayed, cur, loc, mx, d_run, kmax, &k, &rkeys, s, pair_coded))) return rc;
             if (k == 0) {  // no key crosses: both blocks stay as they are
                 xg_close(0.0);
                 continue;
