@@ -139,10 +139,26 @@ __device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
 
 template <typename K>
 __device__ __forceinline__ void cx(K& a, K& b) {
-    const K lo = __builtin_elementwise_min(a, b);
-    const K hi = __builtin_elementwise_max(a, b);
-    a = lo;
-    b = hi;
+#ifndef MISORT_CX64_ONECMP
+#define MISORT_CX64_ONECMP 1
+#endif
+    if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP) {
+        // no 64-bit min/max: as min and max each would cost a v_cmp_u64 + 2
+        // v_cndmask, the selects take one compare -- the empty asm hides that
+        // the selected values are the compared ones, so they are not folded
+        // back into umin/umax
+        const bool lt = a < b;
+        asm("" : "+v"(a), "+v"(b));
+        const K lo = lt ? a : b;
+        const K hi = lt ? b : a;
+        a = lo;
+        b = hi;
+    } else {
+        const K lo = __builtin_elementwise_min(a, b);
+        const K hi = __builtin_elementwise_max(a, b);
+        a = lo;
+        b = hi;
+    }
 }
 
 // 16-byte vector load of keys [i0, i0+V); indices >= n read as the sentinel.
@@ -1461,8 +1477,11 @@ void launch_pass(const K* src, K* dst, int64_t n, const Pass& p, bool ord_in, hi
     tm.ntiles = (n + (1 << LT) - 1) >> LT;
     if (p.kind == KIND_TILE_SORT) {
         if constexpr (sizeof(K) == 8) {
-            if (ord_in) launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s, fence, flk);
-            else launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s, fence, flk);
+            if (ord_in) {
+                launch_stream<K, LT, TM_SORT, 0, false, true>(src, dst, n, tm, s, fence, flk);
+            } else {
+                launch_stream<K, LT, TM_SORT, 0, false, false>(src, dst, n, tm, s, fence, flk);
+            }
         } else if (LT == 15 && MISORT_WAVE_SORT && MISORT_WAVE_LEVELS <= 10 && plan_knobs().sort_u32) {
             launch_sort_u32(src, dst, n, s, (uint64_t*)fence, flk);
         } else {

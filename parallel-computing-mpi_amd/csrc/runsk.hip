@@ -66,6 +66,22 @@ struct KTr;
 #ifndef MISORT_MK_WGCU
 #define MISORT_MK_WGCU 0
 #endif
+// The first fence merge levels of a pass as LDS merge levels (k_fence_merge)
+// when set and the pass has at least FENCE_MERGE_MIN_BLOCKS sub-groups; else
+// ranks by binary searches (k_fence_lds), which can split a sub-group over
+// several blocks.  Measured (profiles/r03/ab3): 2^30 u32 66.5 -> 67.0 Gkeys/s,
+// 2^26 61.5 -> 62.1; at 2^24 (64 and 16 sub-groups) the merge was slower
+// (39.0 -> 38.4).
+#ifndef MISORT_FENCE_MERGE
+#define MISORT_FENCE_MERGE 1
+#endif
+constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
+// u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
+// VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
+// (profiles/r03/ab1); 0 = loads into registers, then ds_write.
+#ifndef MISORT_MK_GLDS
+#define MISORT_MK_GLDS 1
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -232,6 +248,58 @@ __global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT
         }
         if (rank < nfg) M[f0 + rank] = v;  // always true for well-formed fences
     }
+}
+
+// The same result by merge levels in LDS: one block per sub-group of S =
+// 2^(wf_log2 + a) fences (the tail padded with all-ones fences, which sort
+// last and are never stored), a levels of pairwise merges, each lane taking
+// FIT consecutive outputs of its pair: a co-rank search, then a chain with
+// end checks.  k_fence_lds ranks every fence by K - 1 binary searches (56
+// dependent LDS reads per fence at K = 8, runs of 256); a merge level costs a
+// lane about 2 log2(S) reads for FIT outputs.
+constexpr int FIT = 8;
+template <typename FT>
+__global__ __launch_bounds__(1024) void k_fence_merge(const FT* __restrict__ F, FT* __restrict__ M, int64_t nf,
+                                                      int wf_log2, int a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sraw[];
+    FT* sf = reinterpret_cast<FT*>(sraw);
+    const int S = 1 << (wf_log2 + a);
+    const int64_t f0 = (int64_t)blockIdx.x << (wf_log2 + a);
+    const int nfg = (int)((nf - f0) < (int64_t)S ? nf - f0 : (int64_t)S);
+    const int tid = threadIdx.x, NT = blockDim.x;  // NT * FIT == S
+    for (int e = tid; e < S; e += NT) sf[e] = e < nfg ? F[f0 + e] : ~(FT)0;
+    __syncthreads();
+    const int d0 = tid * FIT;
+    FT r[FIT];
+    for (int l = 1; l <= a; ++l) {
+        const int hl = wf_log2 + l - 1;  // log2 of each side of a pair
+        const int base = (d0 >> (hl + 1)) << (hl + 1), W = 1 << hl, d = d0 - base;
+        const FT* A = sf + base;
+        const FT* B = A + W;
+        int lo = d > W ? d - W : 0, hi = d < W ? d : W;
+        while (lo < hi) {  // first i with A[i] > B[d - 1 - i] (A first on ties; fences are distinct)
+            const int mid = (lo + hi) >> 1;
+            if (A[mid] < B[d - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+        }
+        int ia = lo, ib = d - lo;
+        FT av = A[ia < W ? ia : W - 1], bv = B[ib < W ? ib : W - 1];
+#pragma unroll
+        for (int k = 0; k < FIT; ++k) {
+            const bool ta = ia < W && (ib >= W || av < bv);
+            r[k] = ta ? av : bv;
+            ia += ta;
+            ib += !ta;
+            const FT x = ta ? A[ia < W ? ia : W - 1] : B[ib < W ? ib : W - 1];
+            av = ta ? x : av;
+            bv = ta ? bv : x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < FIT; ++k) sf[d0 + k] = r[k];
+        __syncthreads();
+    }
+    for (int e = tid; e < nfg; e += NT) M[f0 + e] = sf[e];  // coalesced
 }
 
 // Chunk index -> (group, chunk within the group), and the group's first chunk.
@@ -733,7 +801,10 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
         if constexpr (sizeof(KEY) == 4) {
             r[k] = min(h, g);
             o = max(h, g);
-        } else {  // no 64-bit min/max: selects on the one compare
+        } else {  // no 64-bit min/max: selects on the compare (the compiler
+                  // emits umin + umax, two v_cmp_u64; hiding the compared values
+                  // from it, as cx<u64> does, measured 5 % slower here:
+                  // 2.52 -> 2.64 ms per 16-way pass at 2^29, profiles/r03/ab2)
             r[k] = keep ? h : g;
             o = keep ? g : h;
         }
@@ -776,19 +847,32 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
         const uint32_t* offp = d->off + part * IT;
         const uint32_t* lap = d->la + part * IT;
         uint32_t off[IT], la[IT];
-        KEY x[IT];
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             off[j] = offp[j];
             la[j] = lap[j];
         }
+        if constexpr (MISORT_MK_GLDS && sizeof(KEY) == 4) {
+            // straight into LDS: a wave's part of a row is 64 consecutive LDS
+            // words from a wave-uniform base (global_load_lds_dword writes
+            // base + 4 * lane), so the row's slot plus the wave's first lane
+            const int wl0 = __builtin_amdgcn_readfirstlane(lt & ~63);
 #pragma unroll
-        for (int j = 0; j < IT; ++j)
-            if (lt < (int)(la[j] & 0xFFFF))
-                x[j] = __builtin_nontemporal_load((const KEY*)(gsrc + off[j]) + (uint32_t)lt);
+            for (int j = 0; j < IT; ++j)
+                if (lt < (int)(la[j] & 0xFFFF))
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)((const KEY*)(gsrc + off[j]) + (uint32_t)lt),
+                        (__attribute__((address_space(3))) void*)(lds_t<KEY>*)(s + (la[j] >> 16) + wl0), 4, 0, 0);
+        } else {
+            KEY x[IT];
 #pragma unroll
-        for (int j = 0; j < IT; ++j)
-            if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
+            for (int j = 0; j < IT; ++j)
+                if (lt < (int)(la[j] & 0xFFFF))
+                    x[j] = __builtin_nontemporal_load((const KEY*)(gsrc + off[j]) + (uint32_t)lt);
+#pragma unroll
+            for (int j = 0; j < IT; ++j)
+                if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
+        }
         if (tid < K * G) {  // the sentinels after every segment
             const int r = tid / G;
             s[d->o[r + 1] + r * G + (tid - r * G)] = MAXK;
@@ -997,9 +1081,15 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             const size_t lds = ((size_t)1 << (wf_log2 + a)) * sizeof(FT);
             const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
             // >= 512 blocks where the sub-groups are few (each loads its whole sub-group)
-            int split = 1;
-            while (split < 8 && nb0 * split < 512 && ((int64_t)1 << (wf_log2 + a)) / (split * 2) >= 1024) split *= 2;
-            k_fence_lds<FT><<<(unsigned)(nb0 * split), 1024, lds, s>>>(F, y, nf, wf_log2, a, split);
+            if (MISORT_FENCE_MERGE && nb0 >= FENCE_MERGE_MIN_BLOCKS) {
+                k_fence_merge<FT><<<(unsigned)nb0, (unsigned)(((int64_t)1 << (wf_log2 + a)) / FIT), lds, s>>>(
+                    F, y, nf, wf_log2, a);
+            } else {
+                int split = 1;
+                while (split < 8 && nb0 * split < 512 && ((int64_t)1 << (wf_log2 + a)) / (split * 2) >= 1024)
+                    split *= 2;
+                k_fence_lds<FT><<<(unsigned)(nb0 * split), 1024, lds, s>>>(F, y, nf, wf_log2, a, split);
+            }
             x = y;
         }
         for (int l = a; l < LK; ++l, --left) {
