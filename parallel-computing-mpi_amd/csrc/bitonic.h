@@ -137,11 +137,16 @@ __device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
     return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
 }
 
-template <typename K>
-__device__ __forceinline__ void cx(K& a, K& b) {
+// u64 compare-exchanges on one v_cmp_u64 (cx); register stages batch their
+// compares ahead of the selects (reg_stages_c).
 #ifndef MISORT_CX64_ONECMP
 #define MISORT_CX64_ONECMP 1
 #endif
+#ifndef MISORT_CX64_BATCH
+#define MISORT_CX64_BATCH 1
+#endif
+template <typename K>
+__device__ __forceinline__ void cx(K& a, K& b) {
     if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP) {
         // no 64-bit min/max: as min and max each would cost a v_cmp_u64 + 2
         // v_cndmask, the selects take one compare -- the empty asm hides that
@@ -348,9 +353,34 @@ __device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
 #pragma unroll
     for (int r = TOP; r > TOP - CNT; --r) {
         const bool fl = FLIP && r == TOP;
+        if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP && MISORT_CX64_BATCH) {
+            // u64: the stage's 16 compares first, then the selects (cx<u64>
+            // one pair at a time waits 2 cycles between each compare and its
+            // selects)
+            bool lt[16];
+            int q = 0;
 #pragma unroll
-        for (int c = 0; c < 32; ++c)
-            if (!(c & (1 << r))) cx(v[c], v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))]);
+            for (int c = 0; c < 32; ++c)
+                if (!(c & (1 << r))) lt[q++] = v[c] < v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))];
+#pragma unroll
+            for (int c = 0; c < 32; ++c)
+                if (!(c & (1 << r))) asm("" : "+v"(v[c]), "+v"(v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))]));
+            q = 0;
+#pragma unroll
+            for (int c = 0; c < 32; ++c) {
+                if (c & (1 << r)) continue;
+                K& a = v[c];
+                K& b = v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))];
+                const bool l = lt[q++];
+                const K lo = l ? a : b, hi = l ? b : a;
+                a = lo;
+                b = hi;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 32; ++c)
+                if (!(c & (1 << r))) cx(v[c], v[fl ? (c ^ ((2 << r) - 1)) : (c | (1 << r))]);
+        }
     }
 }
 
