@@ -52,12 +52,12 @@ enum misort_status {
 /* Kernel families reported by the per-launch profiler. */
 enum misort_kernel_kind {
     MISORT_K_TILE_SORT = 0,   /* levels 1..LT in one LDS tile            */
-    MISORT_K_GLOBAL = 1,      /* fused large-stride HBM pass             */
-    MISORT_K_TILE_MERGE = 2,  /* in-tile strides of one merge level      */
+    MISORT_K_GLOBAL = 1,      /* retired (round 3): network ROWS pass    */
+    MISORT_K_TILE_MERGE = 2,  /* retired (round 3): network merge pass   */
     MISORT_K_MERGE_SPLIT = 3, /* device compare-split (psort.cc:116-164) */
     MISORT_K_OTHER = 4,
-    MISORT_K_SPAN = 5,        /* tail of one level + head of the next    */
-    MISORT_K_WIDE = 6,        /* ROWS strides in a 2^16-key register tile */
+    MISORT_K_SPAN = 5,        /* retired (round 3): network SPAN pass    */
+    MISORT_K_WIDE = 6,        /* retired (round 3): network wide pass    */
     MISORT_K_RUN_MERGE = 7,   /* one merge level: runs 2^hi -> 2^(hi+1)  */
     MISORT_K_EXCHANGE = 8,    /* compare-split exchange leg (splitter samples, RCCL
                                  send/recv, codec), device time between events */
@@ -253,7 +253,7 @@ int misort_profile_stage(misort_ctx* ctx, int stage, int64_t* count, double* exc
  * (at most 2^20 are kept).  For per-pass roofline figures. */
 int misort_profile_trace(misort_ctx* ctx, int max, int* kinds, double* ms, double* bytes);
 
-/* log2 of the LDS tile (keys) used for a key width of 4 or 8 bytes. */
+/* log2 of the SORT tile (keys) used for a key width of 4 or 8 bytes. */
 int misort_tile_log2(int key_bytes);
 
 /* The HBM pass plan of a local sort of n keys (key_bytes 4 or 8), for tools
@@ -263,10 +263,10 @@ int misort_tile_log2(int key_bytes);
 int misort_plan(int64_t n, int key_bytes, int* passes, int max_passes);
 
 /* Tooling: average device time (ms, HIP events on the context stream) of ONE
- * HBM pass of the given shape (kind/hi/R/flip as misort_plan reports them)
- * over n keys, alternating in -> out and out -> in for `reps` launches.  The
- * keys are scrambled by it (a single pass is not a sort).  Feeds the
- * planner's measured cost table (tools/pass_costs.py). */
+ * HBM pass of the given shape (kind MISORT_K_TILE_SORT, MISORT_K_RUN_MERGE or
+ * MISORT_K_RUN_MERGE4; hi/R as misort_plan reports them) over n keys,
+ * alternating in -> out and out -> in for `reps` launches.  A merge pass
+ * assumes ascending runs of 2^hi keys; other input is scrambled, not sorted. */
 int misort_pass_probe(misort_ctx* ctx, int dtype, const void* in, void* out, int64_t n, int kind,
                       int hi, int r, int flip, int reps, float* ms);
 

@@ -11,12 +11,12 @@ namespace misort {
 // Kernel families, used for per-launch profiling (HIP events) and reporting.
 enum Kind : int {
     KIND_TILE_SORT = 0,   // levels 1..LT inside one LDS tile
-    KIND_GLOBAL = 1,      // R fused large-stride stages, registers only
-    KIND_TILE_MERGE = 2,  // strides < tile of one level, LDS tile
+    KIND_GLOBAL = 1,      // retired (round 3): network ROWS pass
+    KIND_TILE_MERGE = 2,  // retired (round 3): network in-tile merge pass
     KIND_MERGE_SPLIT = 3, // compare-split merge (keep lowest/highest n)
     KIND_OTHER = 4,       // f64 transform, fills, checks
-    KIND_SPAN = 5,        // tail of one level + head of the next, row tile
-    KIND_WIDE = 6,        // ROWS strides in a 2^16-key register tile (u32)
+    KIND_SPAN = 5,        // retired (round 3): network SPAN pass
+    KIND_WIDE = 6,        // retired (round 3): network wide ROWS pass
     KIND_RUNS = 7,        // one merge level: runs of 2^hi keys -> runs of 2^(hi+1)
     KIND_EXCHANGE = 8,    // compare-split exchange leg (samples, RCCL send/recv, codec); not a kernel
     KIND_RUNSK = 9,       // R merge levels in one pass: runs of 2^hi -> 2^(hi+R), 2^R-way (runsk.hip)
@@ -56,9 +56,8 @@ template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                       LaunchHook* hook, const StageIO* io = nullptr);
 
-// One HBM pass of the given shape (kind KIND_TILE_SORT / KIND_GLOBAL /
-// KIND_SPAN / KIND_TILE_MERGE, hi, R, flip as in the plan) over n keys: the
-// pass-cost probe behind the planner's cost table.
+// One HBM pass of a plan's shape over n keys (kind KIND_TILE_SORT, KIND_RUNS
+// or KIND_RUNSK; hi, R as in the plan): probes and tests.
 template <typename K>
 hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int flip, hipStream_t s);
 

@@ -12,32 +12,11 @@ PlanKnobs::PlanKnobs() {
     auto env = [](const char* k, int& v) {
         if (const char* e = getenv(k)) v = atoi(e);
     };
-    env("MISORT_TILE_LOG2", tile_u32);
-    env("MISORT_ROWS_TILE_LOG2", rows_tile_u32);
-    env("MISORT_RMAX", rmax);
     env("MISORT_PERSIST", persist);
-    env("MISORT_GRID_MULT", grid_mult);
-    env("MISORT_PINGPONG", pingpong);
-    env("MISORT_SPAN", span);
-    env("MISORT_COST_TABLE", cost_table);
-    env("MISORT_ROW_BYTES_LOG2", row_bytes_log2);
-    env("MISORT_WIDE", wide);
-    env("MISORT_TILE_LOG2_U64", tile_u64);
-    env("MISORT_ROWS_TILE_LOG2_U64", rows_tile_u64);
     env("MISORT_PERSIST_U64", persist_u64);
-    env("MISORT_SORT_U32", sort_u32);
-    env("MISORT_MERGE_FROM", merge_from_u32);
-    env("MISORT_MERGE_FROM_U64", merge_from_u64);
-    env("MISORT_MERGE_MIN_LOG2", merge_min_log2_u32);
+    env("MISORT_GRID_MULT", grid_mult);
     env("MISORT_MULTIWAY", multiway);
     env("MISORT_MULTIWAY_U64", multiway_u64);
-    if (tile_u64 != 13) tile_u64 = 14;
-    if (rows_tile_u64 != 13 && tile_u64 == 14) rows_tile_u64 = 14;
-    if (tile_u64 != 14) rows_tile_u64 = 13;
-    if (tile_u32 != 14) tile_u32 = 15;
-    if (rows_tile_u32 != 14 && tile_u32 == 15) rows_tile_u32 = 15;
-    if (tile_u32 != 15) rows_tile_u32 = 14;
-    if (rmax < 1) rmax = 1;
     if (grid_mult < 1) grid_mult = 1;
 }
 
@@ -46,27 +25,12 @@ const PlanKnobs& plan_knobs() {
     return k;
 }
 
-// Tile size per key type (log2 keys of the SORT/MERGE tile).
-int tile_log2(int key_bytes) {
-    const PlanKnobs& kn = plan_knobs();
-    return key_bytes == 4 ? kn.tile_u32 : kn.tile_u64;
-}
+// SORT tile per key type (log2 keys).
+int tile_log2(int key_bytes) { return key_bytes == 4 ? KT<uint32_t>::LT : KT<uint64_t>::LT; }
 
 int plan_passes(int64_t n, int key_bytes, int* out, int max) {
     if (n <= 0) return 0;
-    constexpr int S = KT<uint32_t>::LT_SMALL;
-    const PlanKnobs& kn = plan_knobs();
-    const bool big = kn.big(key_bytes), rbig = kn.rbig(key_bytes);
-    std::vector<Pass> ps;
-    if (key_bytes == 4) {
-        ps = big && rbig ? plan_for<uint32_t, S + 1, S + 1>(n)
-             : big       ? plan_for<uint32_t, S + 1, S>(n)
-                         : plan_for<uint32_t, S, S>(n);
-    } else {
-        ps = big && rbig ? plan_for<uint64_t, S, S>(n)
-             : big       ? plan_for<uint64_t, S, S - 1>(n)
-                         : plan_for<uint64_t, S - 1, S - 1>(n);
-    }
+    const std::vector<Pass>& ps = key_bytes == 4 ? plan_for<uint32_t>(n) : plan_for<uint64_t>(n);
     const int np = (int)ps.size();
     for (int i = 0; i < np && i < max; ++i) {
         out[4 * i + 0] = ps[i].kind;

@@ -1743,9 +1743,7 @@ int misort_pass_probe(misort_ctx* c, int dtype, const void* in, void* out, int64
                       int r, int flip, int reps, float* ms) {
     if (!c || (dtype != MISORT_U32 && dtype != MISORT_U64) || n <= 0 || !in || !out || in == out || reps < 1 || !ms)
         return fail(MISORT_E_INVALID, "bad pass_probe arguments");
-    if (kind != misort::KIND_TILE_SORT && kind != misort::KIND_GLOBAL && kind != misort::KIND_SPAN &&
-        kind != misort::KIND_TILE_MERGE && kind != misort::KIND_WIDE && kind != misort::KIND_RUNS &&
-        kind != misort::KIND_RUNSK)
+    if (kind != misort::KIND_TILE_SORT && kind != misort::KIND_RUNS && kind != misort::KIND_RUNSK)
         return fail(MISORT_E_INVALID, "bad pass kind");
     hipStream_t s = c->stream;
     hipEvent_t e0, e1;

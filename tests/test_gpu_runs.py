@@ -6,10 +6,10 @@ the SORT tile: 2-way levels (runs.hip) and 2^lk-way passes of lk levels each
 * One merge level (misort_pass_probe, kind run_merge) on inputs made of
   ascending runs of 2^hi keys, ragged tails included, is compared bit for bit
   with numpy: each pair of runs sorted.
-* Full local sorts under MISORT_MERGE_FROM / MISORT_MERGE_FROM_U64 (0: the
-  bitonic network only; later levels: network then merges) and the merge tile
-  knobs MISORT_RUN_IT / MISORT_RUN_NT run in child processes (the planner knobs are read once
-  per process) against np.sort."""
+* Full local sorts (SORT tile, then merge passes) under the pass-width knobs
+  MISORT_MULTIWAY / MISORT_MULTIWAY_U64 and the merge tile knobs MISORT_RUN_IT
+  / MISORT_RUN_NT run in child processes (the planner knobs are read once per
+  process) against np.sort."""
 import os
 import subprocess
 import sys
@@ -188,32 +188,33 @@ ctx.close()
 
 
 @pytest.mark.parametrize("kb,env,n", [
-    (4, {"MISORT_MERGE_FROM": "0"}, (1 << 22) + 4099),
-    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 22) + 4099),
-    (4, {"MISORT_MERGE_FROM": "19"}, 1 << 23),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_IT": "32"}, (1 << 21) + 77),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "256"}, (1 << 21) + 77),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
-    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
-    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
-    (4, {"MISORT_MERGE_FROM": "15", "MISORT_MULTIWAY": "4"}, (1 << 25) + 3),  # 4 + 3 + 3 levels (16-way)
-    (4, {"MISORT_MERGE_FROM": "15"}, 3 * (1 << 23) + 5),
-    (4, {"MISORT_MERGE_FROM": "15"}, (1 << 17) + 1),
-    (8, {"MISORT_MERGE_FROM_U64": "0"}, (1 << 21) + 4099),
-    (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 21) + 4099),
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_IT": "32"}, (1 << 20) + 5),
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_RUN_NT": "512"}, (1 << 20) + 5),
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "0"}, (1 << 21) + 4099),  # 2-way passes
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "2"}, (1 << 21) + 4099),
-    (8, {"MISORT_MERGE_FROM_U64": "13", "MISORT_MULTIWAY_U64": "3"}, (1 << 22) + 3),
-    (8, {"MISORT_MERGE_FROM_U64": "13"}, (1 << 25) + 12345),  # chained 8-way passes, u128 fence merges
+    (4, {}, (1 << 22) + 4099),
+    (4, {}, 1 << 23),
+    (4, {"MISORT_RUN_IT": "32"}, (1 << 21) + 77),
+    (4, {"MISORT_RUN_NT": "256"}, (1 << 21) + 77),
+    (4, {"MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
+    (4, {"MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),
+    (4, {"MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
+    (4, {}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
+    (4, {}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
+    (4, {"MISORT_MULTIWAY": "4"}, (1 << 25) + 3),  # 4 + 3 + 3 levels (16-way)
+    (4, {}, 3 * (1 << 23) + 5),
+    (4, {}, (1 << 17) + 1),  # one level past the tile: a 2-way pass
+    (4, {}, (1 << 16) + 3),
+    (8, {}, (1 << 21) + 4099),
+    (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
+    (8, {"MISORT_RUN_NT": "512"}, (1 << 20) + 5),
+    (8, {"MISORT_MULTIWAY_U64": "0"}, (1 << 21) + 4099),  # 2-way passes
+    (8, {"MISORT_MULTIWAY_U64": "2"}, (1 << 21) + 4099),
+    (8, {"MISORT_MULTIWAY_U64": "3"}, (1 << 22) + 3),
+    (8, {}, (1 << 25) + 12345),  # chained passes, u128 fence merges
 ])
-def test_full_sort_merge_from(kb, env, n):
+def test_full_sort_merge_passes(kb, env, n):
+    """The whole local sort (SORT tile, then merge passes) under the planner
+    knobs, against np.sort; the plan has the fewest multi-way passes for the
+    levels past the tile (u32: 2^15 keys, u64: 2^13)."""
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
-                        str(kb)], env=dict(os.environ, MISORT_MERGE_MIN_LOG2="0", **env), capture_output=True,
-                       text=True, timeout=240)
+                        str(kb)], env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
     _, count, _, countk, verdict = line.split()
@@ -226,8 +227,4 @@ def test_full_sort_merge_from(kb, env, n):
         assert int(countk) == -(-int(count) // cap)  # the fewest multi-way passes
     else:
         assert int(countk) == 0
-    m0 = int(next(iter(env.values())))
-    if m0 == 0:
-        assert int(count) == 0
-    else:
-        assert int(count) == max(0, (n - 1).bit_length() - m0)
+    assert int(count) == max(0, (n - 1).bit_length() - (15 if kb == 4 else 13))
