@@ -947,10 +947,10 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
             }
         }
     }
+    const int64_t out0 = d->out0;
     // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
     // land past the chunk)
-    const int64_t out0 = d->out0;
     const int sh = (int)(out0 & (VK - 1));
     if (pos < len) {
         KEY* q = s + sh + pos;

@@ -437,7 +437,7 @@ class Context:
         _check(lib().misort_profile_reset(self._h))
 
     def pass_probe(self, inp, out, kind, hi, r, flip, reps=5, n=None):
-        """Average ms of one HBM pass of a plan shape (tools/pass_costs.py)."""
+        """Average ms of one HBM pass of a plan shape (tile_sort, run_merge or run_mergek)."""
         ms = ctypes.c_float()
         k = KIND_NAMES.index(kind) if isinstance(kind, str) else int(kind)
         _check(lib().misort_pass_probe(self._h, _dtype_of(inp), _ptr(inp), _ptr(out),

@@ -12,8 +12,9 @@ there (k_runs_merge reads every key exactly once: raw 2.197e9 vs 4.295e9 read
 at 2^30, profiles/r01/pmc30_v11/), so the same doubling applies.  The raw value
 is kept as "read_bytes_raw" and the factor as "fetch_scale".
 The multi-way merge pass (runsk.hip) is k_mergek plus its small planning
-kernels (k_fence_gather on the first multi-way pass, k_fence_lds or the u64
-fence merge levels, k_bounds, k_chunk_desc); "run_mergek" sums them per launch
+kernels (k_fence_gather on the first multi-way pass, k_fence_merge / k_fence_lds
+or the u64 fence merge levels, k_fence_counts, k_scan_totals, k_bounds,
+k_chunk_desc); "run_mergek" sums them per launch
 of k_mergek.  k_mergek's loads are 4 B per lane too, so the same doubling applies.
     WORKLOAD=u32_2e30_n1 tools/traffic.py gpurun_out/pmc30 > profiles/traffic.json
 ("workload" must match bench.py's f"{dtype}_2e{logn}_n{ranks}" for bench to use it).
@@ -40,7 +41,7 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
         m = re.search(r"k_stream<unsigned (?:int|long), (\d+), (\d)", name)
         if m:
             fam = FAMILY[m.group(2)]
-        elif "k_sort_u32" in name:
+        elif "k_sort_u32" in name or "k_sort_tile" in name:
             fam = "tile_sort"
         elif "k_rows_wide" in name:
             fam = "wide_pass"
@@ -52,7 +53,8 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
             fam = "run_partition"
         elif "k_mergek" in name:
             fam = "run_mergek_kernel"
-        elif re.search(r"k_fence_gather|k_fence_lds|k_bounds|k_chunk_desc", name):
+        elif re.search(r"k_fence_gather|k_fence_lds|k_fence_merge|k_fence_counts|k_scan_totals|k_bounds|k_chunk_desc",
+                       name):
             fam = "runk_plan"
         else:
             continue
