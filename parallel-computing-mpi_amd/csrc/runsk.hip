@@ -66,10 +66,6 @@ struct KTr;
 #ifndef MISORT_MK_WGCU
 #define MISORT_MK_WGCU 0
 #endif
-// u64 k_mergek: a lane's outputs as 2 interleaved merge chains when 2.
-#ifndef MISORT_MK_U64_CHAINS
-#define MISORT_MK_U64_CHAINS 1
-#endif
 // The first fence merge levels of a pass as LDS merge levels (k_fence_merge)
 // when set and the pass has at least FENCE_MERGE_MIN_BLOCKS sub-groups; else
 // ranks by binary searches (k_fence_lds), which can split a sub-group over
@@ -820,39 +816,6 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
     }
 }
 
-// The same IT outputs as two interleaved chains of IT/2 (from diagonals d and
-// d + IT/2, each with its own co-rank): two independent LDS read chains per
-// lane for a kernel whose chain is latency-bound (u64: 4 waves per SIMD).
-template <typename KEY, int IT>
-__device__ __forceinline__ void merge_chain2(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
-                                             KEY (&r)[IT]) {
-    constexpr int H = IT / 2;
-    static_assert(IT % 2 == 0, "two equal chains");
-    const int tot = LA + LB;
-    const int d0 = d < tot ? d : tot, d1 = d + H < tot ? d + H : tot;
-    const int i0 = co_rank<KEY>(s, A0, LA, B0, LB, d0, maxr);
-    const int i1 = co_rank<KEY>(s, A0, LA, B0, LB, d1, maxr);
-    uint32_t px0 = lds_addr<KEY>(s + A0 + i0), py0 = lds_addr<KEY>(s + B0 + d0 - i0);
-    uint32_t px1 = lds_addr<KEY>(s + A0 + i1), py1 = lds_addr<KEY>(s + B0 + d1 - i1);
-    KEY h0 = lds_ld<KEY>(px0), g0 = lds_ld<KEY>(py0), h1 = lds_ld<KEY>(px1), g1 = lds_ld<KEY>(py1);
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-        const bool k0 = h0 <= g0, k1 = h1 <= g1;
-        r[k] = k0 ? h0 : g0;
-        r[H + k] = k1 ? h1 : g1;
-        const KEY o0 = k0 ? g0 : h0, o1 = k1 ? g1 : h1;
-        const uint32_t n0 = k0 ? px0 : py0, n1 = k1 ? px1 : py1;
-        py0 = k0 ? py0 : px0;
-        py1 = k1 ? py1 : px1;
-        px0 = n0 + (uint32_t)sizeof(KEY);
-        px1 = n1 + (uint32_t)sizeof(KEY);
-        h0 = lds_ld<KEY>(px0);
-        h1 = lds_ld<KEY>(px1);
-        g0 = o0;
-        g1 = o1;
-    }
-}
-
 // The wave's row part (uniform) and the lane's place in its row.
 template <typename KEY, int LK>
 __device__ __forceinline__ int row_part(int tid) {
@@ -959,10 +922,7 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            if constexpr (sizeof(KEY) == 8 && MISORT_MK_U64_CHAINS == 2)
-                merge_chain2<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
-            else
-                merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         __syncthreads();
         if (lv < LK) {
