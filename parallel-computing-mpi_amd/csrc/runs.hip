@@ -1,12 +1,12 @@
 // runs.hip -- merge levels of the local sort (gfx950): ascending runs of 2^lw
 // keys -> ascending runs of 2^(lw+1), one HBM read + one HBM write per key.
 //
-// The reference's local sort is std::sort (psort.cc:175); the bitonic network of
-// bitonic.h replaces it up to some level, and from there each remaining level
-// of the sort is a pairwise merge of neighbouring runs.  A bitonic level costs
-// about two HBM passes once its strides leave the LDS tile (2^30 u32: 28 passes
-// for levels 16..30); a merge level costs one.  Output is bit-identical: the
-// keys carry no payload, so every correct sort of them writes the same bytes.
+// The reference's local sort is std::sort (psort.cc:175); the bitonic SORT tile
+// of bitonic.h sorts 2^LT-key tiles, and every level above it is a merge of
+// neighbouring runs -- most of them in the multi-way passes of runsk.hip, a
+// level left over (and the fence merges of those passes) here.  Output is
+// bit-identical: the keys carry no payload, so every correct sort of them
+// writes the same bytes.
 //
 // Per level, two launches:
 //   k_runs_partition  32 lanes per output tile: the merge-path co-rank of the
@@ -250,6 +250,12 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
     return hipGetLastError();
 }
 
+// Merge levels over at most RUN_SMALL_N keys use 256-lane tiles when set.
+#ifndef MISORT_RUN_SMALL_TILES
+#define MISORT_RUN_SMALL_TILES 1
+#endif
+constexpr int64_t RUN_SMALL_N = (int64_t)1 << 20;
+
 int env_knob(const char* k) {
     const char* e = getenv(k);
     return e ? atoi(e) : 0;
@@ -278,6 +284,10 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
     if (run_nt_knob() == 256) return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
     if (run_nt_knob() == 512 && fits) return merge_level_it<K, 512, IT>(src, dst, n, lw, s, o0, o1);
     if (run_nt_knob() == 1024 && fits) return merge_level_it<K, 1024, IT>(src, dst, n, lw, s, o0, o1);
+    // small levels (the fence merges of small sorts: 2^17 u64 fences at 2^24 u32
+    // keys are 16 default tiles) take 4x smaller tiles, so more CUs share them
+    if (MISORT_RUN_SMALL_TILES && n <= RUN_SMALL_N && NT > 256 && ((int64_t)1 << lw) >= 256 * IT)
+        return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
     if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1);
     return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);  // runs shorter than the default tile
 }
