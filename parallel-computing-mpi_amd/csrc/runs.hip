@@ -8,7 +8,8 @@
 // bit-identical: the keys carry no payload, so every correct sort of them
 // writes the same bytes.
 //
-// Per level, two launches:
+// Per level, two launches (one on levels of at most 2^20 keys, whose merge
+// workgroups search their own co-ranks: MISORT_RUN_FUSE):
 //   k_runs_partition  32 lanes per output tile: the merge-path co-rank of the
 //                     tile's first output within its pair (a 32-ary search, A
 //                     first on ties);
@@ -94,6 +95,25 @@ __device__ __forceinline__ PairGeo pair_geo(int64_t g, int64_t n, int lw) {
 // load latencies).
 constexpr int PART_LANES = 32;
 
+// The co-rank of output d of one pair (A: na keys, B: nb keys) by one group of
+// PART_LANES lanes (sub: this lane's index in the group, shift: the group's
+// first bit in the wave's ballot).
+template <typename K>
+__device__ __forceinline__ int64_t corank_group(const K* __restrict__ A, const K* __restrict__ B, int64_t d,
+                                                int64_t na, int64_t nb, int sub, int shift) {
+    int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const int64_t step = (hi - lo + PART_LANES - 1) / PART_LANES;
+        const int64_t x = lo + sub * step;
+        const bool t = x < hi && A[x] <= B[d - 1 - x];
+        const int c = __popc((uint32_t)(__ballot(t) >> shift));  // the true points are a prefix
+        const int64_t nhi = lo + c * step;
+        lo = c > 0 ? lo + (c - 1) * step + 1 : lo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    return lo;
+}
+
 template <typename K, int NT, int IT>
 __global__ __launch_bounds__(256) void k_runs_partition(const K* __restrict__ src, int64_t n, int lw, int64_t t0,
                                                         int64_t ntiles, int64_t* __restrict__ co) {
@@ -104,22 +124,15 @@ __global__ __launch_bounds__(256) void k_runs_partition(const K* __restrict__ sr
     const int64_t g0 = (t0 + i) * TILE;
     const PairGeo p = pair_geo(g0, n, lw);
     const K* A = src + p.base;
-    const K* B = A + ((int64_t)1 << lw);
-    const int64_t d = g0 - p.base;
-    int64_t lo = d > p.nb ? d - p.nb : 0, hi = d < p.na ? d : p.na;
-    while (lo < hi) {
-        const int64_t step = (hi - lo + PART_LANES - 1) / PART_LANES;
-        const int64_t x = lo + sub * step;
-        const bool t = x < hi && A[x] <= B[d - 1 - x];
-        const int c = __popc((uint32_t)(__ballot(t) >> shift));  // the true points are a prefix
-        const int64_t nhi = lo + c * step;
-        lo = c > 0 ? lo + (c - 1) * step + 1 : lo;
-        hi = nhi < hi ? nhi : hi;
-    }
+    const int64_t lo = corank_group(A, A + ((int64_t)1 << lw), g0 - p.base, p.na, p.nb, sub, shift);
     if (sub == 0) co[i] = lo;
 }
 
-template <typename K, int NT, int IT>
+// FUSED: the workgroup finds its own two co-ranks (wave 0: lanes 0-31 the
+// tile's first output, lanes 32-63 the one past its last) instead of reading
+// k_runs_partition's -- one launch per level fewer, for levels whose few tiles
+// leave the chip idle anyway.
+template <typename K, int NT, int IT, bool FUSED>
 __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K* __restrict__ dst,
                                                        int64_t n, int lw, int64_t t0,
                                                        const int64_t* __restrict__ co) {
@@ -131,8 +144,26 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
     const int64_t g0 = (t0 + t) * TILE;
     const int64_t g1 = g0 + TILE < n ? g0 + TILE : n;
     const PairGeo p = pair_geo(g0, n, lw);
-    const int64_t i0 = co[t];
-    const int64_t i1 = g1 == p.base + p.na + p.nb ? p.na : co[t + 1];
+    int64_t i0, i1;
+    if constexpr (FUSED) {
+        static_assert(NT >= 64, "wave 0 searches both co-ranks");
+        __shared__ int64_t sco[2];
+        if (tid < 64) {
+            // tiles never straddle pairs (2^lw >= TILE): g1 <= the pair's end,
+            // where the search returns na at once
+            const int h = tid >> 5;
+            const K* A = src + p.base;
+            const int64_t c = corank_group(A, A + ((int64_t)1 << lw), (h ? g1 : g0) - p.base, p.na, p.nb,
+                                           tid & (PART_LANES - 1), h * PART_LANES);
+            if ((tid & (PART_LANES - 1)) == 0) sco[h] = c;
+        }
+        __syncthreads();
+        i0 = sco[0];
+        i1 = sco[1];
+    } else {
+        i0 = co[t];
+        i1 = g1 == p.base + p.na + p.nb ? p.na : co[t + 1];
+    }
     const int64_t j0 = g0 - p.base - i0, j1 = g1 - p.base - i1;
     const int la = (int)(i1 - i0), lb = (int)(j1 - j0), len = la + lb;
     const K* __restrict__ A = src + p.base + i0;
@@ -233,7 +264,8 @@ int64_t* corank_scratch(size_t bytes, hipStream_t s) {
 }
 
 template <typename K, int NT, int IT>
-hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
+hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1,
+                          bool fused = false) {
     constexpr int TILE = NT * IT;
     if (o1 <= 0 || o1 > n) o1 = n;
     if (n <= 0 || o0 >= o1) return hipSuccess;
@@ -241,12 +273,16 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
         (o1 != n && o1 % TILE))
         return hipErrorInvalidValue;
     const int64_t t0 = o0 / TILE, ntiles = (o1 - o0 + TILE - 1) / TILE;
+    if (fused) {
+        k_runs_merge<K, NT, IT, true><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, nullptr);
+        return hipGetLastError();
+    }
     // co[i] for tiles t0 .. t0 + ntiles (the one past the range bounds the last)
     const int64_t nco = t0 + ntiles < (n + TILE - 1) / TILE ? ntiles + 1 : ntiles;
     int64_t* co = corank_scratch((size_t)(ntiles + 1) * sizeof(int64_t), s);
     if (!co) return hipErrorOutOfMemory;
     k_runs_partition<K, NT, IT><<<(unsigned)((nco * PART_LANES + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
-    k_runs_merge<K, NT, IT><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, co);
+    k_runs_merge<K, NT, IT, false><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, co);
     return hipGetLastError();
 }
 
@@ -270,6 +306,13 @@ int run_nt_knob() {
     static const int v = env_knob("MISORT_RUN_NT");
     return v;
 }
+// MISORT_RUN_FUSE: merge workgroups find their own co-ranks (no k_runs_partition
+// launch) on levels of at most RUN_SMALL_N keys (1, the default), never (0) or
+// on every level (2).
+int run_fuse_knob() {
+    static const int v = getenv("MISORT_RUN_FUSE") ? env_knob("MISORT_RUN_FUSE") : 1;
+    return v;
+}
 
 }  // namespace
 
@@ -286,10 +329,11 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
     if (run_nt_knob() == 1024 && fits) return merge_level_it<K, 1024, IT>(src, dst, n, lw, s, o0, o1);
     // small levels (the fence merges of small sorts: 2^17 u64 fences at 2^24 u32
     // keys are 16 default tiles) take 4x smaller tiles, so more CUs share them
+    const bool fuse = run_fuse_knob() == 2 || (run_fuse_knob() == 1 && n <= RUN_SMALL_N);
     if (MISORT_RUN_SMALL_TILES && n <= RUN_SMALL_N && NT > 256 && ((int64_t)1 << lw) >= 256 * IT)
-        return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
-    if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1);
-    return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);  // runs shorter than the default tile
+        return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse);
+    if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1, fuse);
+    return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse);  // runs shorter than the default tile
 }
 
 template hipError_t merge_level<uint32_t>(const uint32_t*, uint32_t*, int64_t, int, hipStream_t, int64_t,
