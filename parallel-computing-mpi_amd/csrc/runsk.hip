@@ -484,57 +484,32 @@ __device__ __forceinline__ int64_t interp(KEY v, KEY ka, KEY kb, int64_t a, int6
     }
 }
 
-// One thread per (bounds slot, run): the start of chunk t of group g in run r
-// (a position within the run), or the run's length for the group's end slot.
+// The start of chunk t of group g in run r (a position within the run), or
+// the run's length for the group's end slot (t = the group's chunk count).
 // Run r's fences before the chunk-start fence f come from the scanned counts;
 // the keys before f lie among the FG positions after the last of them.
 template <typename KEY>
-__global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
-                         const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
-                         const int* __restrict__ bsum, int cpb, Geo geo, int64_t nslots,
-                         int64_t* __restrict__ bounds, bool line) {
+__device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                               const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                               const int* __restrict__ bsum, int cpb, const Geo& geo, int64_t g, int64_t t, int r,
+                               bool line) {
     typedef typename KTr<KEY>::F FT;
-    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= (nslots << geo.lk)) return;
-    const int64_t s = id >> geo.lk;
-    const int r = (int)(id & (geo.K() - 1));
-    int64_t g, t;
-    if (s < geo.nfull * (geo.kf + 1)) {
-        g = (uint32_t)s / (uint32_t)(geo.kf + 1);
-        t = s - g * (geo.kf + 1);
-    } else {
-        g = geo.nfull;
-        t = s - geo.nfull * (geo.kf + 1);
-    }
     const int64_t base = geo.base(g), W = geo.W(), len = geo.run_len(g, r);
-    if (t == geo.nchunks(g)) {
-        bounds[id] = len;
-        return;
-    }
+    if (t == geo.nchunks(g)) return len;
     const FT f = M[(base >> FG_LOG2) + t * geo.fm];
     const KEY v = (KEY)fkey(f);
     const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (geo.K() - 1));
-    if (r == r0) {
-        bounds[id] = (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
-        return;
-    }
-    if (len == 0) {
-        bounds[id] = 0;
-        return;
-    }
+    if (r == r0) return (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
+    if (len == 0) return 0;
     // fences of run r before f: counts of the group's chunks before chunk t
     const int K = geo.K();
     const int64_t c = g * geo.kf + t, c0 = g * geo.kf;  // the tail group starts at nfull * kf too
     const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / cpb) * K + r]) -
                        (P[c0 * K + r] + bsum[(c0 / cpb) * K + r]);
-    if (lo <= 0) {  // run r's first key comes after f
-        bounds[id] = 0;
-        return;
-    }
-    if (lo > (len + FG - 1) >> FG_LOG2) {  // more fences than the run has: malformed input fences
-        bounds[id] = -1;                    // k_chunk_desc rejects the chunk; no read outside the run
-        return;
-    }
+    if (lo <= 0) return 0;  // run r's first key comes after f
+    if (lo > (len + FG - 1) >> FG_LOG2) return -1;  // more fences than the run has: malformed input
+                                                    // fences; k_chunk_desc rejects the chunk, no read
+                                                    // outside the run
     // keys before f: all of positions <= (lo-1)*FG, none from lo*FG on.  The
     // first position after f (key > v if r < r0, key >= v if r > r0) lies in
     // [a, b]; it is guessed by interpolating v between the window's two
@@ -577,10 +552,7 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
             const KEY k = q[i / (16 / (int)sizeof(KEY))][i % (16 / (int)sizeof(KEY))];
             c += (blk + i >= l0 && blk + i < l1 && (le ? k <= v : k < v)) ? 1 : 0;
         }
-        if (c > 0 && c < l1 - l0) {
-            bounds[id] = l0 + c;
-            return;
-        }
+        if (c > 0 && c < l1 - l0) return l0 + c;
         if (c == 0) {  // the answer is at or before l0
             lo_b = a;
             hi_b = l0;
@@ -627,7 +599,28 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
         if (before(mid)) lo_b = mid + 1;
         else hi_b = mid;
     }
-    bounds[id] = lo_b;
+    return lo_b;
+}
+
+// One thread per (bounds slot, run).
+template <typename KEY>
+__global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                         const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                         const int* __restrict__ bsum, int cpb, Geo geo, int64_t nslots,
+                         int64_t* __restrict__ bounds, bool line) {
+    const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (nslots << geo.lk)) return;
+    const int64_t s = id >> geo.lk;
+    const int r = (int)(id & (geo.K() - 1));
+    int64_t g, t;
+    if (s < geo.nfull * (geo.kf + 1)) {
+        g = (uint32_t)s / (uint32_t)(geo.kf + 1);
+        t = s - g * (geo.kf + 1);
+    } else {
+        g = geo.nfull;
+        t = s - geo.nfull * (geo.kf + 1);
+    }
+    bounds[id] = chunk_bound<KEY>(src, F, M, P, bsum, cpb, geo, g, t, r, line);
 }
 
 // Chunk descriptors: for chunk c, its group's base, its output offset, the
@@ -668,25 +661,56 @@ struct DescHdr {
     uint32_t sb[K];
 };
 
-template <typename KEY, int LK, int DC>
+// PLAN (small sorts, MISORT_PLAN_FUSE): the workgroup computes its chunks'
+// bounds itself (chunk_bound: the DC chunk starts and the end of the last one,
+// lane = (chunk, run)) into LDS, in place of a k_bounds launch.
+template <typename KEY, int LK, int DC, bool PLAN>
 __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo, int64_t nchunks,
-                                                   Desc<KEY, LK>* __restrict__ desc, int* __restrict__ err) {
+                                                   Desc<KEY, LK>* __restrict__ desc, int* __restrict__ err,
+                                                   const KEY* __restrict__ src = nullptr,
+                                                   const typename KTr<KEY>::F* __restrict__ F = nullptr,
+                                                   const typename KTr<KEY>::F* __restrict__ M = nullptr,
+                                                   const int* __restrict__ P = nullptr,
+                                                   const int* __restrict__ bsum = nullptr, int cpb = 0,
+                                                   bool line = false) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NROWS = S::NROWS;
     __shared__ DescHdr<KEY, LK> hdr[DC];
     __shared__ uint8_t seg[DC][NROWS];  // row -> its segment
+    __shared__ int64_t sbd[PLAN ? DC + 1 : 1][K];  // PLAN: item j = the start of chunk cb + j (j = nc: the
+                                                   // slot after chunk cb + nc - 1)
     const int lane = threadIdx.x;
     const int64_t cb = (int64_t)blockIdx.x * DC;
     const int nc = nchunks - cb < DC ? (int)(nchunks - cb) : DC;
+    if constexpr (PLAN) {
+        for (int e = lane; e < (nc + 1) * K; e += DC_NT) {
+            const int j = e / K, r = e - j * K;
+            int64_t g, t;
+            chunk_place(geo, cb + (j < nc ? j : nc - 1), g, t);
+            sbd[j][r] = chunk_bound<KEY>(src, F, M, P, bsum, cpb, geo, g, j < nc ? t : t + 1, r, line);
+        }
+        __syncthreads();
+    }
     if (lane < nc) {
         int64_t g, t;
         chunk_place(geo, cb + lane, g, t);
-        const int64_t* b0 = bounds + K * geo.slot(g, t);
         int64_t st[K], en[K];
+        if constexpr (PLAN) {
+            // the chunk's end: the runs' ends for the group's last chunk, else
+            // the next item (the next chunk's start, or the slot after the block's last)
+            const bool last = t + 1 == geo.nchunks(g);
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
-            st[r] = b0[r];
-            en[r] = b0[K + r];
+            for (int r = 0; r < K; ++r) {
+                st[r] = sbd[lane][r];
+                en[r] = last ? geo.run_len(g, r) : sbd[lane + 1][r];
+            }
+        } else {
+            const int64_t* b0 = bounds + K * geo.slot(g, t);
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                st[r] = b0[r];
+                en[r] = b0[K + r];
+            }
         }
         // bounds outside the runs would be a logic error: never let them address memory
         bool ok = true;
@@ -1107,10 +1131,28 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
-    k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo, nslots,
-                                                                          bounds, (nslots << LK) >= line_min);
-    if (nchunks >= dc16_min) k_chunk_desc<KEY, LK, 16><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks, desc, ew);
-    else k_chunk_desc<KEY, LK, 4><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks, desc, ew);
+    // MISORT_PLAN_FUSE: 1 (default) = bounds inside k_chunk_desc below 4096
+    // chunks, 2 = at every size, 0 = never (profiles/r03/ab_plan: 2^24 u32 43.1
+    // -> 43.9 Gkeys/s; at 2^26, 9362 chunks, 65.2 -> 65.0)
+    static const int plan_fuse = getenv("MISORT_PLAN_FUSE") ? atoi(getenv("MISORT_PLAN_FUSE")) : 1;
+    const bool line = (nslots << LK) >= line_min;
+    if (plan_fuse == 2 || (plan_fuse == 1 && nchunks < 4096)) {
+        if (nchunks >= dc16_min)
+            k_chunk_desc<KEY, LK, 16, true><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(
+                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line);
+        else
+            k_chunk_desc<KEY, LK, 4, true><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(
+                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line);
+    } else {
+        k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo,
+                                                                              nslots, bounds, line);
+        if (nchunks >= dc16_min)
+            k_chunk_desc<KEY, LK, 16, false><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks,
+                                                                                             desc, ew);
+        else
+            k_chunk_desc<KEY, LK, 4, false><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks,
+                                                                                          desc, ew);
+    }
     const unsigned grid = (unsigned)nchunks;
     if (hook) hook->before(KIND_RUNSK_KERNEL, 2.0 * (double)n * sizeof(KEY), s);
     if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);

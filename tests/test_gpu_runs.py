@@ -8,7 +8,7 @@ the SORT tile: 2-way levels (runs.hip) and 2^lk-way passes of lk levels each
   with numpy: each pair of runs sorted.
 * Full local sorts (SORT tile, then merge passes) under the pass-width knobs
   MISORT_MULTIWAY / MISORT_MULTIWAY_U64 and the merge tile knobs MISORT_RUN_IT
-  / MISORT_RUN_NT / MISORT_RUN_FUSE run in child processes (the planner knobs are read once per
+  / MISORT_RUN_NT / MISORT_RUN_FUSE and MISORT_PLAN_FUSE run in child processes (the planner knobs are read once per
   process) against np.sort."""
 import os
 import subprocess
@@ -201,7 +201,8 @@ ctx.close()
     (4, {}, 3 * (1 << 23) + 5),
     (4, {}, (1 << 17) + 1),  # one level past the tile: a 2-way pass
     (4, {}, (1 << 16) + 3),
-    (4, {"MISORT_RUN_FUSE": "0"}, (1 << 24) + 999),  # fence merges with k_runs_partition
+    (4, {"MISORT_RUN_FUSE": "0", "MISORT_PLAN_FUSE": "0"}, (1 << 24) + 999),  # k_runs_partition, k_bounds
+    (4, {"MISORT_PLAN_FUSE": "2"}, (1 << 26) + 12345),  # bounds inside k_chunk_desc<16>
     (4, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),  # every 2-way level fused
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
@@ -211,6 +212,8 @@ ctx.close()
     (8, {"MISORT_MULTIWAY_U64": "3"}, (1 << 22) + 3),
     (8, {}, (1 << 25) + 12345),  # chained passes, u128 fence merges
     (8, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY_U64": "0"}, (1 << 21) + 4099),
+    (8, {"MISORT_PLAN_FUSE": "0"}, (1 << 22) + 3),
+    (8, {"MISORT_PLAN_FUSE": "2"}, (1 << 25) + 12345),
 ])
 def test_full_sort_merge_passes(kb, env, n):
     """The whole local sort (SORT tile, then merge passes) under the planner
