@@ -663,7 +663,11 @@ struct DescHdr {
 
 // PLAN (small sorts, MISORT_PLAN_FUSE): the workgroup computes its chunks'
 // bounds itself (chunk_bound: the DC chunk starts and the end of the last one,
-// lane = (chunk, run)) into LDS, in place of a k_bounds launch.
+// lane = (chunk, run)) into LDS, in place of a k_bounds launch.  nbs > 0: bsum
+// holds the RAW block totals of the nbs fence-count blocks (nbs * K <=
+// PLAN_SCAN_MAX) and every workgroup scans them in LDS, in place of a
+// k_scan_totals launch (a few KB of L2 reads per workgroup).
+constexpr int PLAN_SCAN_MAX = 2048;
 template <typename KEY, int LK, int DC, bool PLAN>
 __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict__ bounds, Geo geo, int64_t nchunks,
                                                    Desc<KEY, LK>* __restrict__ desc, int* __restrict__ err,
@@ -672,22 +676,51 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
                                                    const typename KTr<KEY>::F* __restrict__ M = nullptr,
                                                    const int* __restrict__ P = nullptr,
                                                    const int* __restrict__ bsum = nullptr, int cpb = 0,
-                                                   bool line = false) {
+                                                   bool line = false, int nbs = 0) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NROWS = S::NROWS;
     __shared__ DescHdr<KEY, LK> hdr[DC];
     __shared__ uint8_t seg[DC][NROWS];  // row -> its segment
     __shared__ int64_t sbd[PLAN ? DC + 1 : 1][K];  // PLAN: item j = the start of chunk cb + j (j = nc: the
                                                    // slot after chunk cb + nc - 1)
+    __shared__ int sbs[PLAN ? PLAN_SCAN_MAX : 1];  // PLAN, nbs > 0: the scanned block totals
     const int lane = threadIdx.x;
     const int64_t cb = (int64_t)blockIdx.x * DC;
     const int nc = nchunks - cb < DC ? (int)(nchunks - cb) : DC;
     if constexpr (PLAN) {
+        const int* bs = bsum;
+        if (nbs > 0) {
+            // exclusive scan over blocks, per run: lane = (segment, run), NSEG
+            // segments of consecutive blocks per run, a shuffle scan of the
+            // segment sums across the lanes of one run
+            static_assert(DC_NT % K == 0, "whole runs per wave");
+            constexpr int NSEG = DC_NT / K;
+            for (int e = lane; e < nbs * K; e += DC_NT) sbs[e] = bsum[e];
+            __syncthreads();
+            const int r = lane % K, sg = lane / K, rps = (nbs + NSEG - 1) / NSEG;
+            const int b0 = sg * rps < nbs ? sg * rps : nbs, b1 = b0 + rps < nbs ? b0 + rps : nbs;
+            int sum = 0;
+            for (int b = b0; b < b1; ++b) sum += sbs[b * K + r];
+            int inc = sum;
+#pragma unroll
+            for (int o = 1; o < NSEG; o <<= 1) {
+                const int u = __shfl_up(inc, o * K, DC_NT);
+                inc += sg >= o ? u : 0;
+            }
+            int ex = inc - sum;
+            for (int b = b0; b < b1; ++b) {
+                const int v = sbs[b * K + r];
+                sbs[b * K + r] = ex;
+                ex += v;
+            }
+            __syncthreads();
+            bs = sbs;
+        }
         for (int e = lane; e < (nc + 1) * K; e += DC_NT) {
             const int j = e / K, r = e - j * K;
             int64_t g, t;
             chunk_place(geo, cb + (j < nc ? j : nc - 1), g, t);
-            sbd[j][r] = chunk_bound<KEY>(src, F, M, P, bsum, cpb, geo, g, j < nc ? t : t + 1, r, line);
+            sbd[j][r] = chunk_bound<KEY>(src, F, M, P, bs, cpb, geo, g, j < nc ? t : t + 1, r, line);
         }
         __syncthreads();
     }
@@ -1127,22 +1160,27 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
     if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
-    k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
     // MISORT_PLAN_FUSE: 1 (default) = bounds inside k_chunk_desc below 4096
     // chunks, 2 = at every size, 0 = never (profiles/r03/ab_plan: 2^24 u32 43.1
     // -> 43.9 Gkeys/s; at 2^26, 9362 chunks, 65.2 -> 65.0)
+    // MISORT_PLAN_SCAN: 1 (default) = a fused descriptor kernel scans the
+    // fence-count block totals itself when they fit PLAN_SCAN_MAX, 0 = never
     static const int plan_fuse = getenv("MISORT_PLAN_FUSE") ? atoi(getenv("MISORT_PLAN_FUSE")) : 1;
+    static const int plan_scan = getenv("MISORT_PLAN_SCAN") ? atoi(getenv("MISORT_PLAN_SCAN")) : 1;
     const bool line = (nslots << LK) >= line_min;
-    if (plan_fuse == 2 || (plan_fuse == 1 && nchunks < 4096)) {
+    const bool fuse = plan_fuse == 2 || (plan_fuse == 1 && nchunks < 4096);
+    const int nbs = fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
+    if (nbs == 0) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
+    if (fuse) {
         if (nchunks >= dc16_min)
             k_chunk_desc<KEY, LK, 16, true><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(
-                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line);
+                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line, nbs);
         else
             k_chunk_desc<KEY, LK, 4, true><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(
-                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line);
+                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line, nbs);
     } else {
         k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo,
                                                                               nslots, bounds, line);

@@ -8,7 +8,7 @@ the SORT tile: 2-way levels (runs.hip) and 2^lk-way passes of lk levels each
   with numpy: each pair of runs sorted.
 * Full local sorts (SORT tile, then merge passes) under the pass-width knobs
   MISORT_MULTIWAY / MISORT_MULTIWAY_U64 and the merge tile knobs MISORT_RUN_IT
-  / MISORT_RUN_NT / MISORT_RUN_FUSE and MISORT_PLAN_FUSE run in child processes (the planner knobs are read once per
+  / MISORT_RUN_NT / MISORT_RUN_FUSE, MISORT_PLAN_FUSE and MISORT_PLAN_SCAN run in child processes (the planner knobs are read once per
   process) against np.sort."""
 import os
 import subprocess
@@ -203,6 +203,7 @@ ctx.close()
     (4, {}, (1 << 16) + 3),
     (4, {"MISORT_RUN_FUSE": "0", "MISORT_PLAN_FUSE": "0"}, (1 << 24) + 999),  # k_runs_partition, k_bounds
     (4, {"MISORT_PLAN_FUSE": "2"}, (1 << 26) + 12345),  # bounds inside k_chunk_desc<16>
+    (4, {"MISORT_PLAN_SCAN": "0"}, (1 << 23) + 77),  # fused bounds, block totals by k_scan_totals
     (4, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),  # every 2-way level fused
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
