@@ -550,7 +550,8 @@ struct HookScope {
 
 // fence/flk: see final_store (null: no fences).
 template <typename K, int LT, bool ORD>
-void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence = nullptr, int flk = 0) {
+void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence = nullptr, int flk = 0,
+                      hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     typedef TileGeo<K, LT> G;
     static int64_t cap = 0;  // resident workgroups
     const int64_t ntiles = (n + G::T - 1) >> LT;
@@ -565,8 +566,12 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
     const int64_t want = persist ? cap * plan_knobs().grid_mult : ntiles;
     const int64_t grid = ntiles < want ? ntiles : want;
     if (grid <= 0) return;
-    if (persist) k_sort_tile<K, LT, ORD, true><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, ntiles, fence, flk);
-    else k_sort_tile<K, LT, ORD, false><<<(unsigned)grid, G::NT, 0, s>>>(in, out, n, ntiles, fence, flk);
+    if (persist)
+        launch_timed(k_sort_tile<K, LT, ORD, true>, dim3((unsigned)grid), dim3(G::NT), 0, s, ea, eb, in, out, n, ntiles,
+                     fence, flk);
+    else
+        launch_timed(k_sort_tile<K, LT, ORD, false>, dim3((unsigned)grid), dim3(G::NT), 0, s, ea, eb, in, out, n,
+                     ntiles, fence, flk);
 }
 
 // ------------------------------------------------ u32 SORT pass kernel
@@ -650,8 +655,9 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
 }
 
 // fence/flk: see final_store (null: no fences).
+// ea/eb: timing events carried by the first / last launch (null: none).
 inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
-                            int flk = 0) {
+                            int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     static int64_t cap = 0;
     const int64_t nfull = n >> 15;
     const bool persist = plan_knobs().persist_sort(4);
@@ -662,13 +668,21 @@ inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStr
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<true, true>, 1024, 0);
         cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
     }
+    const bool tail = (nfull << 15) < n;
     if (nfull > 0) {
         const int64_t want = persist ? cap * plan_knobs().grid_mult : nfull;
         const int64_t grid = nfull < want ? nfull : want;
-        if (persist) k_sort_u32<true, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, nfull, 0, fence, flk);
-        else k_sort_u32<false, true><<<(unsigned)grid, 1024, 0, s>>>(in, out, n, nfull, 0, fence, flk);
+        hipEvent_t b = tail ? nullptr : eb;
+        if (persist)
+            launch_timed(k_sort_u32<true, true>, dim3((unsigned)grid), dim3(1024), 0, s, ea, b, in, out, n, nfull,
+                         (int64_t)0, fence, flk);
+        else
+            launch_timed(k_sort_u32<false, true>, dim3((unsigned)grid), dim3(1024), 0, s, ea, b, in, out, n, nfull,
+                         (int64_t)0, fence, flk);
     }
-    if ((nfull << 15) < n) k_sort_u32<false, false><<<1, 1024, 0, s>>>(in, out, n, nfull + 1, nfull, fence, flk);
+    if (tail)
+        launch_timed(k_sort_u32<false, false>, dim3(1), dim3(1024), 0, s, nfull > 0 ? nullptr : ea, eb, in, out, n,
+                     nfull + 1, nfull, fence, flk);
 }
 
 // ------------------------------------------------ the local-sort plan
@@ -718,13 +732,14 @@ const std::vector<Pass>& plan_for(int64_t n) {
 }
 
 template <typename K>
-void launch_sort(const K* src, K* dst, int64_t n, bool ord_in, hipStream_t s, void* fence = nullptr, int flk = 0) {
+void launch_sort(const K* src, K* dst, int64_t n, bool ord_in, hipStream_t s, void* fence = nullptr, int flk = 0,
+                 hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     constexpr int LT = KT<K>::LT;
     if constexpr (sizeof(K) == 8) {
-        if (ord_in) launch_sort_tile<K, LT, true>(src, dst, n, s, fence, flk);
-        else launch_sort_tile<K, LT, false>(src, dst, n, s, fence, flk);
+        if (ord_in) launch_sort_tile<K, LT, true>(src, dst, n, s, fence, flk, ea, eb);
+        else launch_sort_tile<K, LT, false>(src, dst, n, s, fence, flk, ea, eb);
     } else {
-        launch_sort_u32(src, dst, n, s, (uint64_t*)fence, flk);
+        launch_sort_u32(src, dst, n, s, (uint64_t*)fence, flk, ea, eb);
     }
 }
 
@@ -742,11 +757,15 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
     // the SORT pass writes the first multi-way pass's fences (no gather pass)
     // unless it runs chunk by chunk (host staging)
     const bool sort_fences = np > 1 && ps[1].kind == KIND_RUNSK && ps[1].hi == LT && !(io && io->before_first);
+    // a binding hook times the passes by events their kernels carry (host
+    // staging's chunked passes keep marker events)
+    const bool bind = hook && hook->binds() && !(io && (io->before_first || io->after_last));
+    if (bind) hook->bind_reset();
     for (int i = 0; i < np; ++i) {
         // pass i writes `out` iff an even number of passes follow it
         K* dst = ((np - 1 - i) & 1) == 0 ? out : scratch;
         const Pass& p = ps[i];
-        HookScope hs(hook, p.kind, bytes, s);
+        HookScope hs(bind ? nullptr : hook, p.kind, bytes, s);
         if (p.kind == KIND_RUNSK) {
             const bool prevk = i > 0 && (ps[i - 1].kind == KIND_RUNSK || (i == 1 && sort_fences));
             const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
@@ -775,14 +794,17 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
                 if (cout && io->after_last(k0, k1, s)) return hipErrorUnknown;
             }
         } else if (runs) {
-            const hipError_t e = merge_level<K>(src, dst, n, p.hi, s);
+            const hipError_t e = merge_level<K>(src, dst, n, p.hi, s, 0, 0, bind ? hook : nullptr);
             if (e != hipSuccess) return e;
-        } else if (i == 0 && sort_fences) {
-            void* f = mergek_fence_buffer(n, (int)sizeof(K), 0, s);
-            if (!f) return hipErrorOutOfMemory;
-            launch_sort<K>(src, dst, n, ord_in, s, f, ps[1].R);
         } else {
-            launch_sort<K>(src, dst, n, ord_in, s);
+            hipEvent_t ea = nullptr, eb = nullptr;
+            if (bind) (void)hook->bind(KIND_TILE_SORT, -1, bytes, &ea, &eb);
+            void* f = nullptr;
+            if (i == 0 && sort_fences) {
+                f = mergek_fence_buffer(n, (int)sizeof(K), 0, s);
+                if (!f) return hipErrorOutOfMemory;
+            }
+            launch_sort<K>(src, dst, n, ord_in, s, f, f ? ps[1].R : 0, ea, eb);
         }
         src = dst;
     }

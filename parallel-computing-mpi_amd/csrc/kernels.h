@@ -1,6 +1,7 @@
 // kernels.h -- internal launch interface of the gfx950 bitonic kernels
 // (kernels.hip).  Not part of the public C-ABI (include/misort.h).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,11 +28,35 @@ enum Kind : int {
 // Per-launch hook: called before and after every kernel launch of a sort with
 // the kernel kind and its algorithmic HBM bytes (each key read once and
 // written once).  nullptr = no profiling.
+//
+// A hook that binds() times the local sort's passes by events the kernels
+// carry themselves (hipExtLaunchKernelGGL start/stop: the dispatch's own
+// timestamps, no marker packets between the kernels): bind() hands out the
+// events for the next launch (either may be null); kernel_kind >= 0 records
+// that launch, pass_kind >= 0 the pass it ends (from the end of this sort's
+// previous pass; bind_reset() starts a sort), both -1 binds a tick (the stop
+// of the launch before a recorded one, where the hook times a launch from the
+// previous one's end).
 struct LaunchHook {
     virtual void before(Kind k, double bytes, hipStream_t s) = 0;
     virtual void after(Kind k, hipStream_t s) = 0;
+    virtual bool binds() const { return false; }
+    virtual void bind_reset() {}
+    virtual bool bind(int kernel_kind, int pass_kind, double bytes, hipEvent_t* start, hipEvent_t* stop) {
+        (void)kernel_kind, (void)pass_kind, (void)bytes;
+        *start = *stop = nullptr;
+        return false;
+    }
     virtual ~LaunchHook() = default;
 };
+
+// A kernel launch carrying timing events (either may be null), or a plain one.
+template <typename F, typename... Args>
+inline void launch_timed(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, hipEvent_t start,
+                         hipEvent_t stop, Args... args) {
+    if (start || stop) hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, start, stop, 0u, args...);
+    else kernel<<<grid, block, shmem, s>>>(args...);
+}
 
 // Chunked first/last pass of a local sort, for host staging that overlaps the
 // PCIe copies with the sort (misort_sort_host).  The SORT pass runs chunk by
@@ -79,8 +104,10 @@ hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, in
 // 2^lw keys (the last may be short), dst gets the ascending runs of 2^(lw+1).
 // Only output keys [o0, o1) are written (o0 a multiple of 4096, o1 of 4096 or
 // n; o1 <= 0 means n): the chunked last pass of host staging.  src != dst.
+// hook: a binding hook times the level's merge launch as a KIND_RUNS pass.
 template <typename K>
-hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0);
+hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0 = 0, int64_t o1 = 0,
+                       LaunchHook* hook = nullptr);
 
 // lk merge levels in one HBM pass (runsk.hip, u32 and u64, lk = 1..4): src holds
 // ascending runs of 2^lw keys, dst gets ascending runs of 2^(lw+lk) (2^lk-way

@@ -265,7 +265,7 @@ int64_t* corank_scratch(size_t bytes, hipStream_t s) {
 
 template <typename K, int NT, int IT>
 hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1,
-                          bool fused = false) {
+                          bool fused = false, LaunchHook* hook = nullptr) {
     constexpr int TILE = NT * IT;
     if (o1 <= 0 || o1 > n) o1 = n;
     if (n <= 0 || o0 >= o1) return hipSuccess;
@@ -273,8 +273,11 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
         (o1 != n && o1 % TILE))
         return hipErrorInvalidValue;
     const int64_t t0 = o0 / TILE, ntiles = (o1 - o0 + TILE - 1) / TILE;
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (hook && hook->binds()) (void)hook->bind(-1, KIND_RUNS, 2.0 * (double)n * sizeof(K), &ea, &eb);
     if (fused) {
-        k_runs_merge<K, NT, IT, true><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, nullptr);
+        launch_timed(k_runs_merge<K, NT, IT, true>, dim3((unsigned)ntiles), dim3(NT), 0, s, ea, eb, src, dst, n, lw,
+                     t0, (const int64_t*)nullptr);
         return hipGetLastError();
     }
     // co[i] for tiles t0 .. t0 + ntiles (the one past the range bounds the last)
@@ -282,7 +285,8 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
     int64_t* co = corank_scratch((size_t)(ntiles + 1) * sizeof(int64_t), s);
     if (!co) return hipErrorOutOfMemory;
     k_runs_partition<K, NT, IT><<<(unsigned)((nco * PART_LANES + 255) / 256), 256, 0, s>>>(src, n, lw, t0, nco, co);
-    k_runs_merge<K, NT, IT, false><<<(unsigned)ntiles, NT, 0, s>>>(src, dst, n, lw, t0, co);
+    launch_timed(k_runs_merge<K, NT, IT, false>, dim3((unsigned)ntiles), dim3(NT), 0, s, ea, eb, src, dst, n, lw, t0,
+                 (const int64_t*)co);
     return hipGetLastError();
 }
 
@@ -317,29 +321,30 @@ int run_fuse_knob() {
 }  // namespace
 
 template <typename K>
-hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1) {
+hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, int64_t o0, int64_t o1,
+                       LaunchHook* hook) {
     constexpr int IT = RunKT<K>::IT, NT = RunKT<K>::NT;
     if (lw < 0 || lw > 40) return hipErrorInvalidValue;
-    if (run_it_knob() == 2 * IT) return merge_level_it<K, 256, 2 * IT>(src, dst, n, lw, s, o0, o1);
+    if (run_it_knob() == 2 * IT) return merge_level_it<K, 256, 2 * IT>(src, dst, n, lw, s, o0, o1, false, hook);
     if (run_it_knob() == IT / 2 && ((int64_t)1 << lw) >= 1024 * (IT / 2))
-        return merge_level_it<K, 1024, IT / 2>(src, dst, n, lw, s, o0, o1);  // same tile, half the keys per lane
+        return merge_level_it<K, 1024, IT / 2>(src, dst, n, lw, s, o0, o1, false, hook);  // same tile, half the keys per lane
     const bool fits = ((int64_t)1 << lw) >= 1024 * IT;  // runs no shorter than the largest tile
-    if (run_nt_knob() == 256) return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1);
-    if (run_nt_knob() == 512 && fits) return merge_level_it<K, 512, IT>(src, dst, n, lw, s, o0, o1);
-    if (run_nt_knob() == 1024 && fits) return merge_level_it<K, 1024, IT>(src, dst, n, lw, s, o0, o1);
+    if (run_nt_knob() == 256) return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, false, hook);
+    if (run_nt_knob() == 512 && fits) return merge_level_it<K, 512, IT>(src, dst, n, lw, s, o0, o1, false, hook);
+    if (run_nt_knob() == 1024 && fits) return merge_level_it<K, 1024, IT>(src, dst, n, lw, s, o0, o1, false, hook);
     // small levels (the fence merges of small sorts: 2^17 u64 fences at 2^24 u32
     // keys are 16 default tiles) take 4x smaller tiles, so more CUs share them
     const bool fuse = run_fuse_knob() == 2 || (run_fuse_knob() == 1 && n <= RUN_SMALL_N);
     if (MISORT_RUN_SMALL_TILES && n <= RUN_SMALL_N && NT > 256 && ((int64_t)1 << lw) >= 256 * IT)
-        return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse);
-    if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1, fuse);
-    return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse);  // runs shorter than the default tile
+        return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);
+    if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);
+    return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);  // runs shorter than the default tile
 }
 
 template hipError_t merge_level<uint32_t>(const uint32_t*, uint32_t*, int64_t, int, hipStream_t, int64_t,
-                                          int64_t);
+                                          int64_t, LaunchHook*);
 template hipError_t merge_level<uint64_t>(const uint64_t*, uint64_t*, int64_t, int, hipStream_t, int64_t,
-                                          int64_t);
-template hipError_t merge_level<u128>(const u128*, u128*, int64_t, int, hipStream_t, int64_t, int64_t);
+                                          int64_t, LaunchHook*);
+template hipError_t merge_level<u128>(const u128*, u128*, int64_t, int, hipStream_t, int64_t, int64_t, LaunchHook*);
 
 }  // namespace misort

@@ -1174,28 +1174,48 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const bool fuse = plan_fuse == 2 || (plan_fuse == 1 && nchunks < 4096);
     const int nbs = fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
     if (nbs == 0) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
-    if (fuse) {
-        if (nchunks >= dc16_min)
-            k_chunk_desc<KEY, LK, 16, true><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(
-                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line, nbs);
-        else
-            k_chunk_desc<KEY, LK, 4, true><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(
-                nullptr, geo, nchunks, desc, ew, src, F, M, cnt, bsum, cpb, line, nbs);
-    } else {
+    if (!fuse)
         k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo,
                                                                               nslots, bounds, line);
+    // the launch before k_mergek: a binding hook's tick (its end starts k_mergek's record)
+    hipEvent_t ta = nullptr, tb = nullptr;
+    if (hook && hook->binds()) (void)hook->bind(-1, -1, 0.0, &ta, &tb);
+    const dim3 g16((unsigned)((nchunks + 15) / 16)), g4((unsigned)((nchunks + 3) / 4));
+    const int* P0 = cnt;
+    const FT* F0 = F;
+    const FT* M0 = M;
+    if (fuse) {
         if (nchunks >= dc16_min)
-            k_chunk_desc<KEY, LK, 16, false><<<(unsigned)((nchunks + 15) / 16), DC_NT, 0, s>>>(bounds, geo, nchunks,
-                                                                                             desc, ew);
+            launch_timed(k_chunk_desc<KEY, LK, 16, true>, g16, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)nullptr, geo,
+                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs);
         else
-            k_chunk_desc<KEY, LK, 4, false><<<(unsigned)((nchunks + 3) / 4), DC_NT, 0, s>>>(bounds, geo, nchunks,
-                                                                                          desc, ew);
+            launch_timed(k_chunk_desc<KEY, LK, 4, true>, g4, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)nullptr, geo,
+                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs);
+    } else {
+        if (nchunks >= dc16_min)
+            launch_timed(k_chunk_desc<KEY, LK, 16, false>, g16, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)bounds,
+                         geo, nchunks, desc, ew, (const KEY*)nullptr, (const FT*)nullptr, (const FT*)nullptr,
+                         (const int*)nullptr, (const int*)nullptr, 0, false, 0);
+        else
+            launch_timed(k_chunk_desc<KEY, LK, 4, false>, g4, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)bounds, geo,
+                         nchunks, desc, ew, (const KEY*)nullptr, (const FT*)nullptr, (const FT*)nullptr,
+                         (const int*)nullptr, (const int*)nullptr, 0, false, 0);
     }
     const unsigned grid = (unsigned)nchunks;
-    if (hook) hook->before(KIND_RUNSK_KERNEL, 2.0 * (double)n * sizeof(KEY), s);
-    if (lk_next > 0) k_mergek<KEY, LK, true><<<grid, S::NT, 0, s>>>(src, dst, desc, Fn, lw + LK, lk_next);
-    else k_mergek<KEY, LK, false><<<grid, S::NT, 0, s>>>(src, dst, desc, nullptr, 0, 0);
-    if (hook) hook->after(KIND_RUNSK_KERNEL, s);
+    // a binding hook: the launch carries its own events and ends the pass's
+    // record; else marker events around it (nested in the pass's)
+    const double kb = 2.0 * (double)n * sizeof(KEY);
+    hipEvent_t ea = nullptr, eb = nullptr;
+    const bool bound = hook && hook->binds();
+    if (bound) (void)hook->bind(KIND_RUNSK_KERNEL, KIND_RUNSK, kb, &ea, &eb);
+    else if (hook) hook->before(KIND_RUNSK_KERNEL, kb, s);
+    if (lk_next > 0)
+        launch_timed(k_mergek<KEY, LK, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
+                     (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next);
+    else
+        launch_timed(k_mergek<KEY, LK, false>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
+                     (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
+    if (hook && !bound) hook->after(KIND_RUNSK_KERNEL, s);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
     if (probe) {
         // same chunks, outputs to a scratch buffer (the sort is untouched)

@@ -99,6 +99,7 @@ struct Profiler final : misort::LaunchHook {
         hipEvent_t a, b;
         double bytes;
         int stage;  // hypercube stage of parallel_sort (-1: local sort / other)
+        bool own_a = true, own_b = true;  // events another record shares are returned to the pool once
     };
     static constexpr int MAX_STAGES = 64;
     std::vector<hipEvent_t> pool;
@@ -124,10 +125,16 @@ struct Profiler final : misort::LaunchHook {
     std::vector<Rec> open;   // enclosing records (a pass around its kernel)
     bool on = false;
 
+    // Timing-only events skip the system-scope release a default event's
+    // record performs: that write-back of the L2s put ~5 us of idle time behind
+    // every record (2^24 u32: 73 us of a 403 us sort between kernels, rocprofv3
+    // kernel trace, profiles/r03/timeline).  MISORT_PROF_SYSFENCE=1 restores it.
     hipEvent_t take() {
+        static const unsigned flags =
+            getenv("MISORT_PROF_SYSFENCE") && atoi(getenv("MISORT_PROF_SYSFENCE")) ? 0u : hipEventDisableSystemFence;
         if (pool.empty()) {
             hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
             return e;
         }
         hipEvent_t e = pool.back();
@@ -138,6 +145,45 @@ struct Profiler final : misort::LaunchHook {
         if (cur.kind >= 0) open.push_back(cur);
         cur = Rec{k, take(), take(), b, stage};
         if (cur.a) (void)hipEventRecord(cur.a, s);
+    }
+    // Kernel-bound records (the local sort's passes): see LaunchHook.
+    // MISORT_PROF_MARKERS=1 times them by marker events instead.
+    // MISORT_PROF_BIND: 1 = a record's launch carries a start and a stop
+    // event; 2 (default) = launches carry stop events only and a record starts
+    // at the previous stop (its kernel's at the stop of the launch before it,
+    // bound as a tick; a pass's at the end of the previous pass).
+    hipEvent_t last = nullptr;        // the stop of the last bound launch of the current sort
+    hipEvent_t pass_start = nullptr;  // the end of the current sort's previous pass
+    std::vector<hipEvent_t> live;     // bound events, back to the pool at collect()
+    static int bind_mode() {
+        static const int m = getenv("MISORT_PROF_BIND") ? atoi(getenv("MISORT_PROF_BIND")) : 2;
+        return m == 1 ? 1 : 2;
+    }
+    bool binds() const override {
+        static const bool markers = getenv("MISORT_PROF_MARKERS") && atoi(getenv("MISORT_PROF_MARKERS"));
+        return !markers;
+    }
+    void bind_reset() override { last = pass_start = nullptr; }
+    bool bind(int kk, int pk, double b, hipEvent_t* a, hipEvent_t* z) override {
+        *a = *z = nullptr;
+        const bool ticks = bind_mode() == 2;
+        if (kk < 0 && pk < 0 && !ticks) return false;  // a tick: only stop-only binding uses them
+        const bool need_a = (kk >= 0 && (!ticks || !last)) || (pk >= 0 && !pass_start);
+        hipEvent_t ea = need_a ? take() : nullptr, eb = take();
+        if (!eb || (need_a && !ea)) {
+            if (ea) pool.push_back(ea);
+            if (eb) pool.push_back(eb);
+            return false;
+        }
+        if (ea) live.push_back(ea);
+        live.push_back(eb);
+        if (kk >= 0) pending.push_back(Rec{kk, ticks && last ? last : ea, eb, b, stage, false, false});
+        if (pk >= 0) pending.push_back(Rec{pk, pass_start ? pass_start : ea, eb, b, stage, false, false});
+        last = eb;
+        if (pk >= 0 || kk == misort::KIND_TILE_SORT) pass_start = eb;
+        *a = ea;
+        *z = eb;
+        return true;
     }
     void after(misort::Kind, hipStream_t s) override {
         if (cur.b) (void)hipEventRecord(cur.b, s);
@@ -169,10 +215,13 @@ struct Profiler final : misort::LaunchHook {
                     st_bytes[r.stage] += r.bytes;
                 }
             }
-            if (r.a) pool.push_back(r.a);
-            if (r.b) pool.push_back(r.b);
+            if (r.a && r.own_a) pool.push_back(r.a);
+            if (r.b && r.own_b) pool.push_back(r.b);
         }
         pending.clear();
+        for (auto e : live) pool.push_back(e);
+        live.clear();
+        last = pass_start = nullptr;  // back in the pool
         return MISORT_OK;
     }
     void reset() {
@@ -186,9 +235,10 @@ struct Profiler final : misort::LaunchHook {
     }
     ~Profiler() override {
         for (auto& r : pending) {
-            if (r.a) (void)hipEventDestroy(r.a);
-            if (r.b) (void)hipEventDestroy(r.b);
+            if (r.a && r.own_a) (void)hipEventDestroy(r.a);
+            if (r.b && r.own_b) (void)hipEventDestroy(r.b);
         }
+        for (auto e : live) (void)hipEventDestroy(e);
         for (auto e : pool) (void)hipEventDestroy(e);
     }
 };
