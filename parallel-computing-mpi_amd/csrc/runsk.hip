@@ -349,18 +349,33 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 // fences per lane; else (many blocks) the block's SCAN_NT lanes read the fence
 // range coalesced and add each fence to its chunk's counters with an LDS
 // atomic -- 2^30: 41.5 us, the slices' strided loads 107 us.
+// MISORT_FC_U32: one u32 LDS counter per (chunk, run) (the coalesced path's
+// atomics then collide only between lanes of one chunk and run); 0 = the runs'
+// 8-bit fields packed in two u64 words per chunk (a wave's lanes, mostly in one
+// chunk, all add to one word).
+#ifndef MISORT_FC_U32
+#define MISORT_FC_U32 1
+#endif
 constexpr int COUNT_NT = 1024;
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
                                                            int cpb, int* __restrict__ P, int* __restrict__ bsum) {
     __shared__ uint64_t sws[COUNT_NT / 64];
+#if MISORT_FC_U32
+    __shared__ uint32_t sc[SCAN_NT][16];
+#else
     __shared__ unsigned long long sc[SCAN_NT][2];
+#endif
     const int tid = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * cpb, c = c0 + tid;  // cpb <= SCAN_NT chunks per block
     const int64_t c1 = c0 + cpb < nchunks ? c0 + cpb : nchunks;
     const int K = geo.K();
     const int gl = geo.lw + geo.lk;
+#if MISORT_FC_U32
+    for (int i = tid; i < SCAN_NT * 16; i += (int)blockDim.x) (&sc[0][0])[i] = 0u;  // SCAN_NT or COUNT_NT lanes
+#else
     if (tid < SCAN_NT) sc[tid][0] = sc[tid][1] = 0ull;
+#endif
     __syncthreads();
     int64_t g, t;
     chunk_place(geo, c0, g, t);
@@ -378,6 +393,18 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
         ge = ge < geo.nfull ? ge : geo.nfull;
         return ge * geo.kf + (int64_t)((uint32_t)(e - (geo.base(ge) >> FG_LOG2)) / fm) - c0;
     };
+    // a lane's per-run counts of one chunk (8-bit fields of lo8 / hi8) into its LDS counters
+    auto flush = [&](int64_t ch, uint64_t lo8, uint64_t hi8) {
+#if MISORT_FC_U32
+        for (int r = 0; r < K; ++r) {
+            const uint32_t v = (uint32_t)(((r < 8 ? lo8 : hi8) >> (8 * (r & 7))) & 0xFF);
+            if (v) atomicAdd(&sc[ch][r], v);
+        }
+#else
+        if (lo8) atomicAdd(&sc[ch][0], lo8);
+        if (hi8) atomicAdd(&sc[ch][1], hi8);
+#endif
+    };
     if constexpr (SLICES) {
         const int64_t per = (f1 - f0 + COUNT_NT - 1) / COUNT_NT;
         const int64_t e0 = f0 + tid * per, e1 = e0 + per < f1 ? e0 + per : f1;
@@ -386,10 +413,7 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
         for (int64_t e = e0; e < e1; ++e) {
             const int64_t ce = chunk_of(e);
             if (ce != cur) {
-                if (cur >= 0) {
-                    if (lo8) atomicAdd(&sc[cur][0], lo8);
-                    if (hi8) atomicAdd(&sc[cur][1], hi8);
-                }
+                if (cur >= 0) flush(cur, lo8, hi8);
                 cur = ce;
                 lo8 = hi8 = 0;
             }
@@ -398,26 +422,32 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
             if (r < 8) lo8 += one;
             else hi8 += one;
         }
-        if (cur >= 0) {
-            if (lo8) atomicAdd(&sc[cur][0], lo8);
-            if (hi8) atomicAdd(&sc[cur][1], hi8);
-        }
+        if (cur >= 0) flush(cur, lo8, hi8);
     } else if (tid < SCAN_NT) {
         for (int64_t e = f0 + tid; e < f1; e += SCAN_NT) {
             const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
+#if MISORT_FC_U32
+            atomicAdd(&sc[chunk_of(e)][r], 1u);
+#else
             atomicAdd(&sc[chunk_of(e)][r >> 3], 1ull << (8 * (r & 7)));
+#endif
         }
     }
     __syncthreads();
     // scan 4 runs at a time as 16-bit fields of one u64 (block prefixes <=
     // SCAN_NT * FM < 2^16): K/4 block scans instead of K
+#if MISORT_FC_U32
+    auto count_of = [&](int q) { return tid < cpb ? (uint64_t)sc[tid][q] : 0ull; };
+#else
     const uint64_t w8[2] = {tid < cpb ? sc[tid][0] : 0ull, tid < cpb ? sc[tid][1] : 0ull};
+    auto count_of = [&](int q) { return (w8[q >> 3] >> (8 * (q & 7))) & 0xFFull; };
+#endif
     for (int q0 = 0; q0 < K; q0 += 4) {
         uint64_t v = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int q = q0 + j;
-            v |= ((w8[q >> 3] >> (8 * (q & 7))) & 0xFFull) << (16 * j);
+            v |= (q < K ? count_of(q) : 0ull) << (16 * j);
         }
         const uint64_t inc = block_scan_u64(v, sws);
         const int nq = K - q0 < 4 ? K - q0 : 4;
@@ -1158,7 +1188,9 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     }
     const int64_t nb = nbk;
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
-    if (nb < 256) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
+    // MISORT_FC_SLICES_MAX (tests): the block count from which the coalesced form counts
+    static const int64_t slices_max = getenv("MISORT_FC_SLICES_MAX") ? atoll(getenv("MISORT_FC_SLICES_MAX")) : 256;
+    if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);

@@ -204,6 +204,8 @@ ctx.close()
     (4, {"MISORT_RUN_FUSE": "0", "MISORT_PLAN_FUSE": "0"}, (1 << 24) + 999),  # k_runs_partition, k_bounds
     (4, {"MISORT_PLAN_FUSE": "2"}, (1 << 26) + 12345),  # bounds inside k_chunk_desc<16>
     (4, {"MISORT_PLAN_SCAN": "0"}, (1 << 23) + 77),  # fused bounds, block totals by k_scan_totals
+    (4, {"MISORT_FC_SLICES_MAX": "0"}, (1 << 23) + 77),  # fence counts by the coalesced (large-sort) form
+    (8, {"MISORT_FC_SLICES_MAX": "0"}, (1 << 22) + 3),
     (4, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),  # every 2-way level fused
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
