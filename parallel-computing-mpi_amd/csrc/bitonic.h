@@ -80,11 +80,16 @@ namespace {
 
 template <typename K>
 struct KT;
+// Probe-only (tools/build_variant.sh): log2 keys of the u32 SORT tile (14: 512
+// lanes, 64 KiB + padding, two workgroups per CU).
+#ifndef MISORT_SORT_LT_U32
+#define MISORT_SORT_LT_U32 15
+#endif
 template <>
 struct KT<uint32_t> {
     static constexpr uint32_t MAX = 0xFFFFFFFFu;
     static constexpr int V = 4;   // keys per 16-byte vector
-    static constexpr int LT = 15; // log2 keys per SORT tile (128 KiB + padding)
+    static constexpr int LT = MISORT_SORT_LT_U32; // log2 keys per SORT tile (15: 128 KiB + padding)
     typedef uint32_t vec __attribute__((ext_vector_type(4)));
 };
 template <>
@@ -586,28 +591,32 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
 // uniform (SGPRs); lanes add 32-bit offsets.
 template <bool FULL>
 __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* in, int64_t tile, int64_t n, int t) {
-    const uint32_t* tb = in + (tile << 15);
+    constexpr int LT = KT<uint32_t>::LT;
+    const uint32_t* tb = in + (tile << LT);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const int e = place<uint32_t, 15>(k, t);
+        const int e = place<uint32_t, LT>(k, t);
         if constexpr (FULL) {
             const KT<uint32_t>::vec x = __builtin_nontemporal_load(reinterpret_cast<const KT<uint32_t>::vec*>(tb + e));
 #pragma unroll
             for (int j = 0; j < 4; ++j) pre[k][j] = x[j];
         } else {
-            load_vec<uint32_t, false>(in, (tile << 15) + e, n, pre[k]);
+            load_vec<uint32_t, false>(in, (tile << LT) + e, n, pre[k]);
         }
     }
 }
 
+constexpr int SORT_U32_NT = TileGeo<uint32_t, KT<uint32_t>::LT>::NT;
+constexpr int SORT_U32_WPE = KT<uint32_t>::LT == 15 ? 1 : TileGeo<uint32_t, KT<uint32_t>::LT>::WAVES_PER_EU;
 template <bool PERSIST, bool FULL>
-__global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, int64_t ntiles,
-                                                      int64_t tile0, uint64_t* fence, int flk) {
+__global__ __launch_bounds__(SORT_U32_NT, SORT_U32_WPE) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n,
+                                                                        int64_t ntiles, int64_t tile0, uint64_t* fence,
+                                                                        int flk) {
     typedef uint32_t K;
-    constexpr int LT = 15;
+    constexpr int LT = KT<uint32_t>::LT;
     typedef TileGeo<K, LT> G;
     constexpr int WL = MISORT_WAVE_LEVELS;
-    static_assert(G::LOADS == 8 && G::NT == 1024 && WL >= 5 && WL <= 10, "u32 SORT tile shape");
+    static_assert(G::LOADS == 8 && (G::NT == 1024 || G::NT == 512) && WL >= 5 && WL <= 10, "u32 SORT tile shape");
     __shared__ K s[lds_words(G::T)];
     int64_t tile = tile0 + blockIdx.x;
     if (tile >= ntiles) return;
@@ -647,7 +656,7 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
-        sort_levels_w<K, WL + 1, MISORT_SORT_TOP>(s, t);
+        sort_levels_w<K, WL + 1, (MISORT_SORT_TOP < LT ? MISORT_SORT_TOP : LT)>(s, t);
         final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
         if constexpr (!PERSIST) break;
         __syncthreads();
@@ -659,29 +668,29 @@ __global__ __launch_bounds__(1024, 1) void k_sort_u32(const uint32_t* in, uint32
 inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
                             int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     static int64_t cap = 0;
-    const int64_t nfull = n >> 15;
+    const int64_t nfull = n >> KT<uint32_t>::LT;
     const bool persist = plan_knobs().persist_sort(4);
     if (persist && cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<true, true>, 1024, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<true, true>, SORT_U32_NT, 0);
         cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
     }
-    const bool tail = (nfull << 15) < n;
+    const bool tail = (nfull << KT<uint32_t>::LT) < n;
     if (nfull > 0) {
         const int64_t want = persist ? cap * plan_knobs().grid_mult : nfull;
         const int64_t grid = nfull < want ? nfull : want;
         hipEvent_t b = tail ? nullptr : eb;
         if (persist)
-            launch_timed(k_sort_u32<true, true>, dim3((unsigned)grid), dim3(1024), 0, s, ea, b, in, out, n, nfull,
+            launch_timed(k_sort_u32<true, true>, dim3((unsigned)grid), dim3(SORT_U32_NT), 0, s, ea, b, in, out, n, nfull,
                          (int64_t)0, fence, flk);
         else
-            launch_timed(k_sort_u32<false, true>, dim3((unsigned)grid), dim3(1024), 0, s, ea, b, in, out, n, nfull,
+            launch_timed(k_sort_u32<false, true>, dim3((unsigned)grid), dim3(SORT_U32_NT), 0, s, ea, b, in, out, n, nfull,
                          (int64_t)0, fence, flk);
     }
     if (tail)
-        launch_timed(k_sort_u32<false, false>, dim3(1), dim3(1024), 0, s, nfull > 0 ? nullptr : ea, eb, in, out, n,
+        launch_timed(k_sort_u32<false, false>, dim3(1), dim3(SORT_U32_NT), 0, s, nfull > 0 ? nullptr : ea, eb, in, out, n,
                      nfull + 1, nfull, fence, flk);
 }
 

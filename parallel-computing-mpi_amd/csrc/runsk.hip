@@ -82,6 +82,9 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
 #endif
+#ifndef MISORT_SORT_LT_U32
+#define MISORT_SORT_LT_U32 15  // the u32 SORT tile (bitonic.h)
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -90,7 +93,7 @@ struct KTr<uint32_t> {
     static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
-    static constexpr int LW_MIN = 15, LWK_MAX = 30;         // runs >= the SORT tile; 32-bit row offsets
+    static constexpr int LW_MIN = MISORT_SORT_LT_U32 < 15 ? MISORT_SORT_LT_U32 : 15, LWK_MAX = 30;  // runs >= the SORT tile; 32-bit row offsets
 };
 static_assert(KTr<uint32_t>::NT == 256 || KTr<uint32_t>::NT == 384 || KTr<uint32_t>::NT == 512 ||
                   KTr<uint32_t>::NT == 1024,

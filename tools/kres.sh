@@ -3,7 +3,7 @@
 #   tools/kres.sh [filter-regex]
 HERE="$(cd "$(dirname "$0")/.." && pwd)"
 C="$HERE/parallel-computing-mpi_amd/csrc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$HERE/include" -I"$C" -c "$C/${KRES_SRC:-kernels.hip}" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$HERE/include" -I"$C" $KRES_FLAGS -c "$C/${KRES_SRC:-kernels.hip}" \
     -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys, subprocess
