@@ -79,6 +79,10 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 // u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
 // VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
 // (profiles/r03/ab1); 0 = loads into registers, then ds_write.
+// k_mergek chunks in one contiguous range per XCD (1) or chunk = block (0).
+#ifndef MISORT_MK_XCD
+#define MISORT_MK_XCD 0
+#endif
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
 #endif
@@ -928,7 +932,15 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
     __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
     KEY* s = tile + PAD;
     const int tid = threadIdx.x;
-    const Desc<KEY, LK>* d = desc + blockIdx.x;
+    uint32_t chunk = blockIdx.x;
+    if constexpr (MISORT_MK_XCD) {
+        // blocks b, b + 8, ... share an XCD (round-robin dispatch): give each
+        // XCD one contiguous range of chunks, so neighbouring chunks' shared
+        // boundary lines meet in one L2 (a bijection for any grid size)
+        const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7, q = nb >> 3, rm = nb & 7;
+        chunk = x * q + (x < rm ? x : rm) + (b >> 3);
+    }
+    const Desc<KEY, LK>* d = desc + chunk;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
         // table entries first (scalar registers), then all its loads
