@@ -1,7 +1,7 @@
 # Round 3, final call: the whole GPU suite, smoke(), the default bench line,
 # and the rocprofv3 kernel stats of the same bench command.
 set -o pipefail
-R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/r03x"; mkdir -p "$O"; cd "$R"
+R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/${OUTDIR:-r03x}"; mkdir -p "$O"; cd "$R"
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --durations=20 --timeout 300 --timeout-method thread > "$O/pytest.log" 2>&1
 rc=$?; echo "pytest rc $rc: $(tail -1 $O/pytest.log)"; [ $rc -eq 0 ] || { tail -30 "$O/pytest.log"; exit $rc; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 || { echo smoke failed; tail -5 "$O/smoke.log"; exit 1; }
