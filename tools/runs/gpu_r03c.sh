@@ -13,5 +13,5 @@ fi
 timeout -k 10 300 python bench.py ${BENCH_ARGS} > "$O/bench.json" 2> "$O/bench.err" || { echo bench failed; tail -5 "$O/bench.err"; exit 1; }
 cat "$O/bench.json"
 [ -n "$SKIP_PROF" ] && exit 0
-OUTDIR=${OUTDIR:-r03c}/prof bash tools/gpu_r02_prof.sh > "$O/prof.txt" 2>&1 || { echo prof failed; tail -20 "$O/prof.txt"; exit 1; }
+OUTDIR=${OUTDIR:-r03c}/prof bash tools/runs/gpu_r02_prof.sh > "$O/prof.txt" 2>&1 || { echo prof failed; tail -20 "$O/prof.txt"; exit 1; }
 cat "$O/prof.txt" | head -120

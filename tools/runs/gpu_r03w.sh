@@ -10,4 +10,4 @@ for args in "" "--logn=28" "--logn=24"; do
   echo "== $args"
   STEPS=$steps OUTDIR=r03w/$tag BENCH_ARGS="$args" RUNS="b15||;b15m4||MISORT_MULTIWAY=4;l14|$V|;l14m3|$V|MISORT_MULTIWAY=3" bash tools/gpu_envab.sh || exit $?
 done
-bash tools/gpu_r03v.sh
+bash tools/runs/gpu_r03v.sh
