@@ -234,6 +234,16 @@ def load_cpu_json(path):
     return cpu
 
 
+def baseline_config(logn, dtype):
+    """The BASELINE.json config a bench workload is (configs[1..4]; config 5 is
+    u64 N = 2^29 - 3 / - 7 over 8 GPUs, so a 2^29 u64 line is its size only)."""
+    if dtype == "u32" and logn in (24, 28, 30):
+        return f"BASELINE config {({24: 2, 28: 3, 30: 4})[logn]}"
+    if dtype == "u64" and logn == 29:
+        return "BASELINE config 5's key type and size (N = 2^29, not 2^29 - 3 / - 7)"
+    return "not a BASELINE config"
+
+
 def load_traffic(workload):
     """Per-launch HBM bytes of this exact workload from the committed rocprofv3
     --pmc summary profiles/traffic_<workload>.json (tools/traffic.py), or None
@@ -532,7 +542,7 @@ def main(argv=None):
             "dtype": args.dtype,
             "data": "synthetic (SplitMix64 keys generated in HBM, seed 0x5EED0003)",
             "config": {"workload": f"bitonic sort 2^{args.logn} {args.dtype} keys "
-                                   f"(BASELINE config {'3/4' if args.logn == 30 else 'custom'})",
+                                   f"({baseline_config(args.logn, args.dtype)})",
                        "keys": n_total, "keys_per_gpu": loc,
                        "algo": args.algo, "local_sort": local_algo,
                        "parallelism": (f"hypercube bitonic, {nranks} GPU(s), RCCL compare-split"

@@ -45,8 +45,11 @@ enum misort_status {
     MISORT_E_NO_COMM = -5,   /* communicator not initialised */
     MISORT_E_CAPACITY = -6,  /* a partner block exceeds max_size (MPI_Sendrecv truncation) */
     MISORT_E_INTERNAL = -7   /* a merge pass rejected its own chunk bounds (a planning bug: the
-                                output is incomplete); reported at the next host sync of the
-                                stream (misort_synchronize, misort_check_sort) */
+                                output is incomplete); reported by the call itself where it
+                                syncs (misort_sort_host), else at the next host sync of the
+                                same stream: misort_synchronize for the context's own stream,
+                                misort_check_sort for the stream it is given (a sort on a
+                                caller's stream is reported there, not by misort_synchronize) */
 };
 
 /* Kernel families reported by the per-launch profiler. */
@@ -77,6 +80,11 @@ int misort_create(int device, misort_ctx** out);
 int misort_destroy(misort_ctx* ctx);
 /* hipStream_t of the context (as void*). */
 void* misort_stream(misort_ctx* ctx);
+/* Waits for the context's own stream (not a caller's stream) and reports a
+ * merge pass's rejected chunk on it (MISORT_E_INTERNAL).  With a communicator,
+ * a wait that follows transport calls is bounded by MISORT_TIMEOUT_S (default
+ * 120 s; a deadline aborts the communicator, MISORT_E_RCCL); a wait on local
+ * work only is not. */
 int misort_synchronize(misort_ctx* ctx);
 
 /* ---- communicator (replaces MPI_COMM_WORLD, psort.cc:107,535-536) -------- */

@@ -778,7 +778,11 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
         if (p.kind == KIND_RUNSK) {
             const bool prevk = i > 0 && (ps[i - 1].kind == KIND_RUNSK || (i == 1 && sort_fences));
             const int lk_next = i + 1 < np && ps[i + 1].kind == KIND_RUNSK ? ps[i + 1].R : 0;
-            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, hook);
+            // a binding hook only while binding (host staging records the pass
+            // by the HookScope marker above; binding there too would record it
+            // twice, from a stale start); a marker hook nests k_mergek's record
+            LaunchHook* kh = bind || !(hook && hook->binds()) ? hook : nullptr;
+            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh);
             if (e != hipSuccess) return e;
             fence_phase ^= 1;
             src = dst;

@@ -86,6 +86,11 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
 #endif
+// The in-LDS merge levels of k_mergek: 0 = one key per LDS read (merge_chain),
+// 1 / 2 = two keys per read (merge_chain_blk; 2: one wide unaligned read).
+#ifndef MISORT_MK_CHAIN
+#define MISORT_MK_CHAIN 0
+#endif
 #ifndef MISORT_SORT_LT_U32
 #define MISORT_SORT_LT_U32 15  // the u32 SORT tile (bitonic.h)
 #endif
@@ -910,6 +915,78 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
     }
 }
 
+// Two consecutive keys at LDS byte address a.  MISORT_MK_CHAIN 2: one
+// ds_read_b64 (u32) / ds_read_b128 (u64) at the key's own alignment -- the
+// type claims the vector's alignment so the compiler selects the single wide
+// read, which the unaligned LDS mode of the HSA queues serves; 1: the
+// compiler's choice for a key-aligned pair (ds_read2_b32 / ds_read2_b64, two
+// LDS accesses).
+template <typename KEY, bool WIDE>
+__device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
+    if constexpr (WIDE) {
+        return *(const __attribute__((address_space(3))) kvec2<KEY>*)(uintptr_t)a;
+    } else {
+        typedef KEY v2 __attribute__((ext_vector_type(2), aligned(sizeof(KEY))));
+        const v2 v = *(const __attribute__((address_space(3))) v2*)(uintptr_t)a;
+        return kvec2<KEY>{v.x, v.y};
+    }
+}
+
+template <typename KEY>
+__device__ __forceinline__ KEY kmin(KEY a, KEY b) {
+    return a < b ? a : b;
+}
+template <typename KEY>
+__device__ __forceinline__ KEY kmax(KEY a, KEY b) {
+    return a < b ? b : a;
+}
+
+// The same IT outputs as merge_chain, two per step from blocks of two keys
+// (a vector merge: Inoue et al., AA-sort).  The lane holds v, the two largest
+// keys it has read and not yet output; each step reads the next two keys of the
+// side whose last read key is the smaller (the other side's last read key is in
+// v, and every unread key of that side is >= it, so the two smallest of v and
+// the block are the next two outputs), then splits v and the block into the
+// lower pair (output) and the upper pair (the new v) -- one LDS read per two
+// outputs.  A side gives at most IT keys, so the G >= IT sentinels after each
+// sequence cover every read.
+template <typename KEY, int IT, bool WIDE>
+__device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                                KEY (&r)[IT]) {
+    static_assert(IT % 2 == 0, "two outputs per step");
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;
+    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    constexpr uint32_t B2 = 2 * sizeof(KEY);
+    uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
+    const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
+    pa += B2;
+    pb += B2;
+    KEY ta = a.y, tb = b.y;
+    KEY l0 = kmin(a.x, b.y), l1 = kmin(a.y, b.x), h0 = kmax(a.x, b.y), h1 = kmax(a.y, b.x);
+    r[0] = kmin(l0, l1);
+    r[1] = kmax(l0, l1);
+    KEY v0 = kmin(h0, h1), v1 = kmax(h0, h1);
+#pragma unroll
+    for (int k = 1; k < IT / 2; ++k) {
+        const bool c = ta <= tb;
+        const uint32_t ad = c ? pa : pb;
+        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(ad);
+        pa = c ? ad + B2 : pa;
+        pb = c ? pb : ad + B2;
+        ta = c ? n.y : ta;
+        tb = c ? tb : n.y;
+        l0 = kmin(v0, n.y);
+        l1 = kmin(v1, n.x);
+        h0 = kmax(v0, n.y);
+        h1 = kmax(v1, n.x);
+        r[2 * k] = kmin(l0, l1);
+        r[2 * k + 1] = kmax(l0, l1);
+        v0 = kmin(h0, h1);
+        v1 = kmax(h0, h1);
+    }
+}
+
 // The wave's row part (uniform) and the lane's place in its row.
 template <typename KEY, int LK>
 __device__ __forceinline__ int row_part(int tid) {
@@ -975,9 +1052,9 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
             for (int j = 0; j < IT; ++j)
                 if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         }
-        if (tid < K * G) {  // the sentinels after every segment
-            const int r = tid / G;
-            s[d->o[r + 1] + r * G + (tid - r * G)] = MAXK;
+        for (int e = tid; e < K * G; e += NT) {  // the sentinels after every segment
+            const int r = e / G;
+            s[d->o[r + 1] + r * G + (e - r * G)] = MAXK;
         }
     }
     __syncthreads();
@@ -1024,7 +1101,10 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            if constexpr (MISORT_MK_CHAIN == 0)
+                merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            else
+                merge_chain_blk<KEY, IT, MISORT_MK_CHAIN == 2>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         __syncthreads();
         if (lv < LK) {
@@ -1034,12 +1114,12 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
 #pragma unroll
                 for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
             }
-            if (tid < P * G) {
-                const int p = tid / G;
+            for (int x = tid; x < P * G; x += NT) {
+                const int p = x / G;
                 int e = 0;
 #pragma unroll
                 for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
-                s[e + (tid - p * G)] = MAXK;
+                s[e + (x - p * G)] = MAXK;
             }
             __syncthreads();
 #pragma unroll

@@ -394,15 +394,26 @@ struct RcclTransport final : Transport {
     // remote failure or the deadline aborts the communicator and returns
     // MISORT_E_RCCL.  Spins briefly (stage waits are usually short), then
     // sleeps between polls.
+    uint64_t drained_calls = 0;  // `calls` at the last wait that drained the stream
     int wait(hipStream_t s) override {
         int rc = usable();
         if (rc) return rc;
+        if (calls == drained_calls) {
+            // no transport call since the stream last drained: only local work
+            // is queued (it may legitimately run longer than the peer deadline,
+            // e.g. under a counter-collecting profiler), so no deadline and no abort
+            HIPCHK(hipStreamSynchronize(s));
+            return MISORT_OK;
+        }
         TRACE("rank %d: waiting on the stream (deadline %.0f s)", rank, peer_timeout_s());
         const auto t0 = std::chrono::steady_clock::now();
         const double lim = peer_timeout_s();
         for (int it = 0;; ++it) {
             const hipError_t q = hipStreamQuery(s);
-            if (q == hipSuccess) return MISORT_OK;
+            if (q == hipSuccess) {
+                drained_calls = calls;
+                return MISORT_OK;
+            }
             if (q != hipErrorNotReady) {
                 abort_all("stream error while waiting for peers");
                 return fail(MISORT_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
@@ -1900,7 +1911,16 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     int64_t four[5];
     if ((rc = fetch(c, s, {{four, mine, 4 * sizeof(int64_t)}}))) return rc;
     const int perr = planning_check(s);
-    if (perr == MISORT_E_HIP) return perr;
+    if (perr == MISORT_E_HIP) {
+        // this rank cannot take part in the gather: abort the communicator so
+        // the peers fail now instead of waiting out their deadline
+        if (p > 1) {
+            const std::string why = g_err;
+            c->tr->abort_all(why.c_str());
+            g_err = why;
+        }
+        return perr;
+    }
     four[4] = perr != MISORT_OK;
     std::vector<int64_t> alli(four, four + 5);
     if (p > 1) {
@@ -2091,9 +2111,11 @@ int misort_sort_host(misort_ctx* c, int dtype, const void* h_in, void* h_out, in
         for (int64_t k0 = 0; k0 < loc; k0 += ch)
             if ((rc = op.push(k0, std::min(loc, k0 + ch), s))) return rc;
     }
-    if ((rc = op.finish())) return rc;
-    if ((rc = sync(c, s))) return rc;
-    return MISORT_OK;
+    if ((rc = op.finish())) return collective_result(c, calls0, rc);
+    if ((rc = sync(c, s))) return collective_result(c, calls0, rc);
+    // a merge pass that rejected its chunk bounds left the output incomplete:
+    // report it here, not on a later unrelated misort_synchronize
+    return collective_result(c, calls0, planning_check(s));
 }
 
 int misort_fill_splitmix(misort_ctx* c, int dtype, void* out, int64_t n, uint64_t seed, int64_t g0,

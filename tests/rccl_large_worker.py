@@ -8,6 +8,9 @@ only the wire is not xGMI).
                                          `raw`: MISORT_COMPRESS=0 + whole-block
                                          exchange, a 4*N/P-byte ncclSend per stage
     rccl_large_worker.py config5         u64 N = 2^29-3 and 2^29-7 ("ref" mix) at P = 8
+    rccl_large_worker.py config5full     the same N with BASELINE config 5's own mix
+                                         ("full": 5 % all-ones keys, the sentinel
+                                         collision, crossing the real exchange)
     rccl_large_worker.py stall|dead      rank 1 stops taking part (sleeps / exits)
                                          after the communicator is up; rank 0 must
                                          get MISORT_E_RCCL within MISORT_TIMEOUT_S
@@ -141,15 +144,16 @@ def main():
             ctx.fill_splitmix(t, c["seed"], g0)
         sort_and_check(f"config4_P{world}{'_raw' if raw else ''}", c["n"], u32_t, fill,
                        c["out_sha256"], c["errors"])
-    elif mode == "config5":
+    elif mode in ("config5", "config5full"):
+        variant = "ref" if mode == "config5" else "full"
         for c in large:
-            if c["config"] != 5 or c["variant"] != "ref" or c["p"] != world:
+            if c["config"] != 5 or c["variant"] != variant or c["p"] != world:
                 continue
 
             def fill(t, g0, cnt, c=c):
                 x = O.u64mix(c["seed"], c["n"], int(c["top"], 16), g0, cnt)
                 t.view(torch.int64).copy_(torch.from_numpy(x.view(np.int64)))
-            sort_and_check(f"config5_N{c['n']}_P{world}", c["n"], u64_t, fill, c["out_sha256"], c["errors"],
+            sort_and_check(f"{mode}_N{c['n']}_P{world}", c["n"], u64_t, fill, c["out_sha256"], c["errors"],
                            c["sizes"])
     else:
         raise SystemExit(f"unknown mode {mode}")

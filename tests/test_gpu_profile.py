@@ -8,7 +8,9 @@ process per setting).
 Either way one sort yields, in pass order, tile_sort, then per multi-way pass
 its k_mergek launch (run_mergek_kernel) and the pass (run_mergek), per 2-way
 pass run_merge; every record is positive, a k_mergek launch is within its pass,
-and the passes add up to no more than the sort's wall time."""
+and the passes add up to no more than the sort's wall time.  A host-staged sort
+(misort_sort_host) records each pass once, by its marker scope (k_mergek's own
+record nests only under marker timing)."""
 import json
 import os
 import subprocess
@@ -43,6 +45,21 @@ for n, kb in ((1 << 24, 4), ((1 << 16) + 3, 4), ((1 << 21) + 5, 8), ((1 << 23) +
     tr = ctx.profile_trace()
     ctx.profile(False)
     out[f"{n}_{kb}"] = {"plan": [p[0] for p in misort.plan(n, kb)], "trace": tr, "wall_ms": wall}
+# host staging (misort_sort_host): its passes are recorded by marker scopes,
+# each exactly once, in plan order
+import numpy as np
+hn = (1 << 22) + 9
+h = np.random.default_rng(1).integers(0, 2**32, hn, dtype=np.uint64).astype(np.uint32)
+ctx.sort_host(h)  # warm
+ctx.profile(True)
+ctx.profile_reset()
+t0 = time.perf_counter()
+r = ctx.sort_host(h)
+wall = (time.perf_counter() - t0) * 1e3
+tr = ctx.profile_trace()
+ctx.profile(False)
+out["host"] = {"plan": [p[0] for p in misort.plan(hn, 4)], "trace": tr, "wall_ms": wall,
+               "sorted": bool(np.array_equal(r, np.sort(h)))}
 print("JSON", json.dumps(out))
 ctx.close()
 """
@@ -56,10 +73,13 @@ def test_pass_records(markers, bind):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads([x for x in r.stdout.splitlines() if x.startswith("JSON")][-1][5:])
+    assert res["host"]["sorted"]
     for key, v in res.items():
         want = []
+        # host staging nests k_mergek's record only under marker timing
+        nest = key != "host" or markers == "1"
         for kind in v["plan"]:
-            want += ["run_mergek_kernel", "run_mergek"] if kind == "run_mergek" else [kind]
+            want += ["run_mergek_kernel", "run_mergek"] if kind == "run_mergek" and nest else [kind]
         trace = v["trace"]
         assert [t[0] for t in trace] == want, key
         assert all(t[1] > 0 for t in trace), (key, trace)

@@ -8,7 +8,10 @@ tests/rccl_large_worker.py).
   2 GiB ncclSend/ncclRecv each way, the reference's MPI_Sendrecv of the whole
   block (psort.cc:121-122, 146-147);
 * config 5, u64 N = 2^29 - 3 (the reference's defective uneven output, 1 error)
-  and 2^29 - 7 at P = 8;
+  and 2^29 - 7 at P = 8, with keys the reference can take as doubles ("ref")
+  and with BASELINE config 5's own mix ("full": 5 % all-ones keys, which
+  collide with the merge passes' MAX sentinels, crossing the real exchange,
+  psort.cc:121-122, 146-147);
 * failure detection: a peer that stalls or dies after the communicator is up
   makes rank 0 fail with MISORT_E_RCCL within MISORT_TIMEOUT_S instead of
   hanging (the reference's alarm(540) watchdog + abort, psort.cc:17,56-65,170),
@@ -78,8 +81,9 @@ def launch(p, args, timeout, extra_env=None):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("p,args", [(2, ["config4"]), (2, ["config4", "raw"]), (8, ["config4"]),
-                                    (8, ["config5"])],
-                         ids=["config4_P2", "config4_P2_raw_whole_block", "config4_P8", "config5_P8"])
+                                    (8, ["config5"]), (8, ["config5full"])],
+                         ids=["config4_P2", "config4_P2_raw_whole_block", "config4_P8", "config5_P8",
+                              "config5_full_P8"])
 def test_rccl_baseline_size(p, args):
     rc, res = launch(p, args, timeout=280)
     assert rc == 0, res
@@ -89,7 +93,7 @@ def test_rccl_baseline_size(p, args):
     if "raw" in args:
         # whole blocks crossed: 2 x 2^29 keys x 4 B sent + received by rank 0
         assert res["results"][0]["rank0_stage_bytes"] == 2 * (1 << 29) * 4
-    if args == ["config5"]:
+    if args[0].startswith("config5"):
         assert len(res["results"]) == 2
 
 

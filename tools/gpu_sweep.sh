@@ -1,5 +1,5 @@
 # Config sweep: GPU parity tests under each config, then the 2^30 bench.
-#   CONFIGS="MISORT_TILE_LOG2=14 MISORT_CHUNK=23,..." (space-separated, comma = several vars)
+#   CONFIGS="MISORT_MULTIWAY=4 MISORT_FC_SLICES_MAX=0,..." (space-separated, comma = several vars)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"; mkdir -p gpurun_out
 i=0
