@@ -66,6 +66,9 @@ struct KTr;
 #ifndef MISORT_MK_WGCU
 #define MISORT_MK_WGCU 0
 #endif
+#ifndef MISORT_MK_IT
+#define MISORT_MK_IT 0  // u32 outputs per lane of a merge level (0: 18 at >= 512 lanes)
+#endif
 // The first fence merge levels of a pass as LDS merge levels (k_fence_merge)
 // when set and the pass has at least FENCE_MERGE_MIN_BLOCKS sub-groups; else
 // ranks by binary searches (k_fence_lds), which can split a sub-group over
@@ -87,9 +90,16 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #define MISORT_MK_GLDS 1
 #endif
 // The in-LDS merge levels of k_mergek: 0 = one key per LDS read (merge_chain),
-// 1 / 2 = two keys per read (merge_chain_blk; 2: one wide unaligned read).
+// 1 / 2 = two keys per read (merge_chain_blk; 1: ds_read2_b32 / ds_read2_b64,
+// 2: one unaligned ds_read_b64 / ds_read_b128).  Measured at 2^30 u32
+// (profiles/r04/ab_chain): k_mergek 1999 -> 1969 us with 1; 2 takes 4329 us
+// -- unaligned wide LDS reads are far slower than their bank model (the SQ
+// counts fewer bank-conflict cycles) -- and u64 with 2 16.7 -> 21.3 ms.
 #ifndef MISORT_MK_CHAIN
-#define MISORT_MK_CHAIN 0
+#define MISORT_MK_CHAIN 1
+#endif
+#ifndef MISORT_MK_CHAIN_U64
+#define MISORT_MK_CHAIN_U64 0
 #endif
 #ifndef MISORT_SORT_LT_U32
 #define MISORT_SORT_LT_U32 15  // the u32 SORT tile (bitonic.h)
@@ -98,7 +108,7 @@ template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
     static constexpr int NT = MISORT_MK_NT;
-    static constexpr int IT = NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
+    static constexpr int IT = MISORT_MK_IT ? MISORT_MK_IT : NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
     static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
@@ -932,23 +942,41 @@ __device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
     }
 }
 
-template <typename KEY>
-__device__ __forceinline__ KEY kmin(KEY a, KEY b) {
-    return a < b ? a : b;
+// The four keys of two ascending pairs (v0 <= v1, n0 <= n1) in order:
+// s0 = min(v0, n0), s3 = max(v1, n1), and with a = max(v0, n0) <= max(v1, n1)
+// the middle two are min(a, min(v1, n1)) and max(a, min(v1, n1)) -- for u32
+// a v_min_u32, v_max_u32, v_min3_u32, v_med3_u32 and v_max_u32; for u64 three
+// compares, each selecting both of its outputs.
+[[maybe_unused]] __device__ __forceinline__ void merge4(uint32_t v0, uint32_t v1, uint32_t n0, uint32_t n1, uint32_t& s0, uint32_t& s1,
+                                       uint32_t& s2, uint32_t& s3) {
+    s0 = min(v0, n0);
+    const uint32_t a = max(v0, n0);
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(s1) : "v"(a), "v"(v1), "v"(n1));  // (not formed from min(min()))
+    s2 = max(min(a, v1), min(max(a, v1), n1));  // v_med3_u32
+    s3 = max(v1, n1);
 }
-template <typename KEY>
-__device__ __forceinline__ KEY kmax(KEY a, KEY b) {
-    return a < b ? b : a;
+[[maybe_unused]] __device__ __forceinline__ void merge4(uint64_t v0, uint64_t v1, uint64_t n0, uint64_t n1, uint64_t& s0, uint64_t& s1,
+                                       uint64_t& s2, uint64_t& s3) {
+    const bool c0 = v0 < n0, c1 = v1 < n1;
+    s0 = c0 ? v0 : n0;
+    const uint64_t a = c0 ? n0 : v0, m = c1 ? v1 : n1;
+    s3 = c1 ? n1 : v1;
+    const bool c2 = a < m;
+    s1 = c2 ? a : m;
+    s2 = c2 ? m : a;
 }
 
 // The same IT outputs as merge_chain, two per step from blocks of two keys
-// (a vector merge: Inoue et al., AA-sort).  The lane holds v, the two largest
-// keys it has read and not yet output; each step reads the next two keys of the
-// side whose last read key is the smaller (the other side's last read key is in
-// v, and every unread key of that side is >= it, so the two smallest of v and
-// the block are the next two outputs), then splits v and the block into the
-// lower pair (output) and the upper pair (the new v) -- one LDS read per two
-// outputs.  A side gives at most IT keys, so the G >= IT sentinels after each
+// (a vector merge, as in Inoue et al.'s AA-sort).  The lane holds v0 <= v1,
+// the two largest keys it has read and not yet output; v1, the largest key
+// read, is the last key read from one side (L), so every unread key of L is
+// >= v1, and the next two outputs are the lowest two of v and the next two
+// keys of the other side (S).  A step reads those two keys (one LDS read),
+// outputs the lowest two of the four and keeps the upper two; when the block's
+// second key exceeds v1 the sides swap roles (the block's side now holds the
+// largest key read).  Five VALU ops of merging and four of pointers per two
+// outputs (u32) -- the one-key chain spends six VALU and an LDS read per
+// output.  A side gives at most IT keys, so the G >= IT sentinels after each
 // sequence cover every read.
 template <typename KEY, int IT, bool WIDE>
 __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
@@ -958,32 +986,22 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     const int dc = d < tot ? d : tot;
     const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
     constexpr uint32_t B2 = 2 * sizeof(KEY);
-    uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
+    const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
     const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
-    pa += B2;
-    pb += B2;
-    KEY ta = a.y, tb = b.y;
-    KEY l0 = kmin(a.x, b.y), l1 = kmin(a.y, b.x), h0 = kmax(a.x, b.y), h1 = kmax(a.y, b.x);
-    r[0] = kmin(l0, l1);
-    r[1] = kmax(l0, l1);
-    KEY v0 = kmin(h0, h1), v1 = kmax(h0, h1);
+    // S: the side whose last read key is the smaller (ties: either)
+    const bool as = a.y <= b.y;
+    uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
+    KEY v0, v1;
+    merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
 #pragma unroll
     for (int k = 1; k < IT / 2; ++k) {
-        const bool c = ta <= tb;
-        const uint32_t ad = c ? pa : pb;
-        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(ad);
-        pa = c ? ad + B2 : pa;
-        pb = c ? pb : ad + B2;
-        ta = c ? n.y : ta;
-        tb = c ? tb : n.y;
-        l0 = kmin(v0, n.y);
-        l1 = kmin(v1, n.x);
-        h0 = kmax(v0, n.y);
-        h1 = kmax(v1, n.x);
-        r[2 * k] = kmin(l0, l1);
-        r[2 * k + 1] = kmax(l0, l1);
-        v0 = kmin(h0, h1);
-        v1 = kmax(h0, h1);
+        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(ps);
+        ps += B2;
+        const bool sw = n.y > v1;
+        merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
+        const uint32_t t = sw ? pl : ps;
+        pl = sw ? ps : pl;
+        ps = t;
     }
 }
 
@@ -1101,10 +1119,11 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            if constexpr (MISORT_MK_CHAIN == 0)
+            constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
+            if constexpr (CH == 0)
                 merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else
-                merge_chain_blk<KEY, IT, MISORT_MK_CHAIN == 2>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+                merge_chain_blk<KEY, IT, CH == 2>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         __syncthreads();
         if (lv < LK) {
