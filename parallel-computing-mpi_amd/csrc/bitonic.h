@@ -11,7 +11,7 @@
 //            sorted by the bitonic network in LDS and registers -- levels 1..LT
 //            in one HBM read and one HBM write per key;
 //   RUNSK    2^lk-way merge passes (runsk.hip): lk merge levels per HBM sweep
-//            (u32: 5 eight-way passes for 2^30 keys past the tile);
+//            (u32, 2^30 keys past the tile: three 16-way passes and one 8-way);
 //   RUNS     a single level left over (or every level, MISORT_MULTIWAY=0):
 //            2-way merge passes (runs.hip).
 // The keys carry no payload, so any correct sort writes the same bytes as the
@@ -50,15 +50,15 @@ namespace misort {
 //   MISORT_PERSIST_U64     the same for the u64 (and f64) SORT pass (default 1);
 //   MISORT_MULTIWAY        u32 merge levels per multi-way pass (runsk.hip,
 //                          2^lk-way, lk <= 4); 0 or 1: one 2-way pass per level;
-//                          -1 (default): see multiway_cap;
+//                          -1 (default): 4 (see multiway_cap);
 //   MISORT_MULTIWAY_U64    the same for u64 (and f64) keys (default 4).
 struct PlanKnobs {
     int persist = 1, persist_u64 = 1, grid_mult = 1;
-    // -1 (default): 3 when the L levels past the SORT tile are a multiple of
-    // 3 (then 8-way passes only), else 4 (the fewest passes) -- measured per
-    // size (profiles/r02/ab_mw_u32): L = 15 (2^30) 8-way 64.1 vs 63.2 Gkeys/s
-    // with 16-way, L = 12 63.5 vs 63.2; L = 10, 11, 13, 14 the fewer passes
-    // win by 4 / 3 / 1.6 / 0.7 %
+    // -1 (default): 4, the fewest passes (up to 16-way) at every size.  Round
+    // 2 had kept 8-way passes where the levels split into threes (L = 12, 15:
+    // 2^27, 2^30); with the two-keys-per-read merge chain the fewest passes win
+    // everywhere (profiles/r04/mw, one box, 2 x 10 sorts each): 2^26 +2.0 %,
+    // 2^27 +1.3 %, 2^28 +3.8 %, 2^29 +2.2 %, 2^30 +0.9 %, 2^31 +0.6 %
     int multiway = -1;
     // u64 (and f64): 128-bit fences, 8192-key chunks at 2 workgroups per CU.
     // 16-way passes measured faster for u64 at every size (profiles/r02/ab_mw:
@@ -70,7 +70,8 @@ struct PlanKnobs {
     int multiway_cap(int kb, int L) const {
         if (kb != 4) return multiway_u64;
         if (multiway >= 0) return multiway;
-        return L % 3 == 0 ? 3 : 4;
+        (void)L;
+        return 4;
     }
     bool persist_sort(int kb) const { return (kb == 4 ? persist : persist_u64) & 1; }
 };

@@ -141,18 +141,34 @@ constexpr int SCAN_NT_MAX = 256;  // chunks per fence-count block (SCAN_NT below
 template <typename KEY, int LK>
 struct Shape {
     typedef KTr<KEY> T;
-    static constexpr int NT = T::NT, IT = T::IT, CAP = T::CAP, G = IT + 1;
+    // the merge chain of the in-LDS levels (MISORT_MK_CHAIN*) and the sentinels
+    // after each sequence: G >= the keys a chain may read past its sequence
+    static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
+    static constexpr int NT = T::NT, IT = T::IT, CAP = T::CAP;
+    // chain 3 merges RN = IT + 2 keys rounded up to even (the lane's IT outputs
+    // after up to two early keys) and reads up to RN + 2 - 2 keys past a
+    // sequence start; chains 0-2 read up to IT
+    static constexpr int RN = CH == 3 ? (IT + 3) & ~1 : IT;
+    static constexpr int G = CH == 3 ? RN + 1 : IT + 1;
+    // level outputs start at lane boundaries; chain 3 also needs even slots
+    static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
+    static_assert(CH != 3 || QA % 2 == 0, "chain 3: even sequence starts");
+    static_assert(CH == 3 || IT % 2 == 0, "chains 0-2: outputs stored as aligned pairs");
+    // LDS slot of segment q (o = its first chunk position): chain 3 reads
+    // aligned pairs, so every sequence starts at an even slot
+    __device__ __host__ static int seg(int o, int q) { return CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G; }
     static constexpr int K = 1 << LK;
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
     static constexpr int RW = LK == 4 ? 64 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
-    static constexpr int NROWS = IT * NR;           // lane slot j of part p holds row j * NR + p
-    static constexpr int LDS_KEYS = PAD + CAP + K * (G + IT) + 16;
+    static constexpr int LS = (T::IT + 1) & ~1;    // load slots per lane (18 at IT = 17 or 18)
+    static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
+    static constexpr int LDS_KEYS = PAD + CAP + K * (G + QA) + 16;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
-    static_assert(CAP + (K / 2) * (G + IT) <= NT * IT, "level layout: pairs at lane boundaries");
-    static_assert(PAD + CAP + K * (G + IT) < 65536, "LDS key index of a row fits 16 bits");
+    static_assert(CAP + (K / 2) * (G + QA) <= NT * IT, "level layout: pairs at lane boundaries");
+    static_assert(PAD + CAP + K * (G + QA) < 65536, "LDS key index of a row fits 16 bits");
 };
 
 template <typename KEY>
@@ -682,8 +698,8 @@ __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F
 // row j = byte offset of its first key from the group base, and how many of
 // its RW keys are real plus the LDS slot the first goes to (segment r's keys
 // start at LDS slot o_r + r*G, leaving G slots for sentinels after each).
-// The tables are stored by part: entry p*IT + j is row j*NR + p, so a wave
-// reads its IT entries as a few wide scalar loads.
+// The tables are stored by part: entry p*LS + j is row j*NR + p, so a wave
+// reads its LS entries as a few wide scalar loads.
 // Validated so that no chunk can address memory outside its group's runs:
 // a bad chunk gets no rows and is left unwritten (the sort then fails its
 // checks).
@@ -835,13 +851,13 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
     for (int e = lane; e < nc * NROWS; e += DC_NT) {
         const int cl = e / NROWS, j = e - cl * NROWS;
         const DescHdr<KEY, LK>& h = hdr[cl];
-        const int row = (j % S::IT) * S::NR + j / S::IT;  // table entry j (stored by part)
+        const int row = (j % S::LS) * S::NR + j / S::LS;  // table entry j (stored by part)
         uint32_t off = 0, la = 0;
         if (row < h.srow[K]) {  // rows past the chunk: no keys
             const int rr = seg[cl][row];
             const int k = row - h.srow[rr], rem = h.sln[rr] - k * S::RW;
             off = h.sb[rr] + (uint32_t)(k * S::RW * (int)sizeof(KEY));
-            la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(h.so[rr] + rr * S::G + k * S::RW) << 16);
+            la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(S::seg(h.so[rr], rr) + k * S::RW) << 16);
         }
         d[cl].off[j] = off;
         d[cl].la[j] = la;
@@ -886,6 +902,34 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     return base;
 }
 
+// co_rank at diagonal d, searched from diagonal d + 1 by the lanes 16..31 of
+// each 32-lane LDS group (MISORT_MK_SKEW): with IT even the lanes' diagonals
+// (IT apart) fall on only 16 of the 32 banks, so every search step that the
+// lanes take at a common base is a 2-way conflict on its B probe (and on its
+// A probe where the bases are d - LB); the one-off skew puts the 32 probes on
+// 32 banks.  The split at d is the split at d + 1 less its larger last key
+// (the d-th output): two more reads for the skewed lanes.
+#ifndef MISORT_MK_SKEW
+#define MISORT_MK_SKEW 1
+#endif
+template <typename KEY>
+__device__ __forceinline__ int co_rank_skew(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
+    if constexpr (!MISORT_MK_SKEW) {
+        return co_rank<KEY>(s, A0, LA, B0, LB, d, maxr);
+    } else {
+        const bool sk = (__lane_id() & 16) && d < LA + LB;
+        const int dq = d + (sk ? 1 : 0);
+        const int iq = co_rank<KEY>(s, A0, LA, B0, LB, dq, maxr);
+        if (!sk) return iq;
+        // the d-th output is max(A[iq - 1], B[dq - iq - 1]) (a side with no key
+        // before the split cannot give it)
+        const int jq = dq - iq;
+        const KEY a = s[A0 + iq - 1], b = s[B0 + jq - 1];
+        const bool fromA = jq == 0 || (iq > 0 && a > b);
+        return fromA ? iq - 1 : iq;
+    }
+}
+
 // IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
 // both followed by sentinels.  A chain holds h, the head of the side it took
 // last, and g, the other side's head: each step outputs min(h, g), keeps
@@ -899,7 +943,7 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
                                             KEY (&r)[IT]) {
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
-    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
     // byte addresses of the two heads (LDS pointers are 32-bit)
     uint32_t px = lds_addr<KEY>(s + A0 + ia), py = lds_addr<KEY>(s + B0 + dc - ia);
     KEY h = lds_ld<KEY>(px), g = lds_ld<KEY>(py);
@@ -984,7 +1028,7 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     static_assert(IT % 2 == 0, "two outputs per step");
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;
-    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
     constexpr uint32_t B2 = 2 * sizeof(KEY);
     const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
     const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
@@ -1003,6 +1047,44 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
         pl = sw ? ps : pl;
         ps = t;
     }
+}
+
+// merge_chain_blk with ALIGNED two-key reads (chain 3: one ds_read_b64 for u32,
+// ds_read_b128 for u64, at the pair's own alignment -- the unaligned forms
+// measured 2.2x slower).  Every sequence starts at an even LDS slot, and the
+// lane starts each side at the aligned pair holding its first key: when that
+// key is the pair's second, the pair's first key is an earlier output -- <=
+// every key this lane outputs (A[ia-1] <= B[ib] by the co-rank, B[ib-1] <
+// A[ia] by its maximality) -- so it leaves the merge first.  The lane merges
+// RN >= IT + 2 keys (even); its outputs are r[ex, ex + IT), ex = the early
+// keys (0..2).  A side gives at most RN keys from its pair, so G >= RN
+// sentinels.  IT may be odd (the lanes' diagonals then fall on distinct banks).
+template <typename KEY, int IT, int RN>
+__device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                              KEY (&r)[RN]) {
+    static_assert(RN % 2 == 0 && RN >= IT + 2, "two outputs per step, two early keys");
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;
+    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ib = dc - ia;
+    constexpr uint32_t B2 = 2 * sizeof(KEY);
+    const uint32_t pa = lds_addr<KEY>(s + A0 + (ia & ~1)), pb = lds_addr<KEY>(s + B0 + (ib & ~1));
+    const kvec2<KEY> a = lds_ld2<KEY, true>(pa), b = lds_ld2<KEY, true>(pb);
+    const bool as = a.y <= b.y;
+    uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
+    KEY v0, v1;
+    merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
+#pragma unroll
+    for (int k = 1; k < RN / 2; ++k) {
+        const kvec2<KEY> n = lds_ld2<KEY, true>(ps);
+        ps += B2;
+        const bool sw = n.y > v1;
+        merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
+        const uint32_t t = sw ? pl : ps;
+        pl = sw ? ps : pl;
+        ps = t;
+    }
+    return (ia & 1) + (ib & 1);
 }
 
 // The wave's row part (uniform) and the lane's place in its row.
@@ -1041,11 +1123,12 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
         // table entries first (scalar registers), then all its loads
         const char* gsrc = (const char*)(src + d->gbase);
         const int part = row_part<KEY, LK>(tid), lt = tid & (S::RW - 1);
-        const uint32_t* offp = d->off + part * IT;
-        const uint32_t* lap = d->la + part * IT;
-        uint32_t off[IT], la[IT];
+        constexpr int LS = S::LS;
+        const uint32_t* offp = d->off + part * LS;
+        const uint32_t* lap = d->la + part * LS;
+        uint32_t off[LS], la[LS];
 #pragma unroll
-        for (int j = 0; j < IT; ++j) {
+        for (int j = 0; j < LS; ++j) {
             off[j] = offp[j];
             la[j] = lap[j];
         }
@@ -1055,36 +1138,39 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
             // base + 4 * lane), so the row's slot plus the wave's first lane
             const int wl0 = __builtin_amdgcn_readfirstlane(lt & ~63);
 #pragma unroll
-            for (int j = 0; j < IT; ++j)
+            for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF))
                     __builtin_amdgcn_global_load_lds(
                         (const __attribute__((address_space(1))) void*)((const KEY*)(gsrc + off[j]) + (uint32_t)lt),
                         (__attribute__((address_space(3))) void*)(lds_t<KEY>*)(s + (la[j] >> 16) + wl0), 4, 0, 0);
         } else {
-            KEY x[IT];
+            KEY x[LS];
 #pragma unroll
-            for (int j = 0; j < IT; ++j)
+            for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF))
                     x[j] = __builtin_nontemporal_load((const KEY*)(gsrc + off[j]) + (uint32_t)lt);
 #pragma unroll
-            for (int j = 0; j < IT; ++j)
+            for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         }
         for (int e = tid; e < K * G; e += NT) {  // the sentinels after every segment
             const int r = e / G;
-            s[d->o[r + 1] + r * G + (e - r * G)] = MAXK;
+            s[S::seg(d->o[r], r) + (d->o[r + 1] - d->o[r]) + (e - r * G)] = MAXK;
         }
     }
     __syncthreads();
     const int len = d->o[K];
-    KEY r[IT];
+    constexpr int CH = S::CH;
+    constexpr int RN = S::RN;  // chain 3: up to two leading keys not the lane's (ex)
+    KEY r[RN];
+    int ex = 0;  // the lane's outputs are r[ex, ex + IT)
     const int pos = tid * IT;
     const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
     // the current level's input sequences (uniform): start and length
     int st[K], ln[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) {
-        st[q] = d->o[q] + q * G;
+        st[q] = S::seg(d->o[q], q);
         ln[q] = d->o[q + 1] - d->o[q];
     }
 #pragma unroll
@@ -1100,7 +1186,7 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
             maxr = mr > maxr ? mr : maxr;
             lp[p] = ln[2 * p] + ln[2 * p + 1];
             qp[p] = qa;
-            qa = (qa + lp[p] + G + IT - 1) / IT * IT;
+            qa = (qa + lp[p] + G + S::QA - 1) / S::QA * S::QA;
         }
         // the lane's pair: the last one starting at or before pos
         int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
@@ -1116,12 +1202,14 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
         }
         const int end = qp[P - 1] + lp[P - 1];
         if (MODE == 1 || (MODE == 2 && lv > 1)) {
+            ex = 0;
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
         } else if (wpos < end) {
-            constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
             if constexpr (CH == 0)
                 merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            else if constexpr (CH == 3)
+                ex = merge_chain_al<KEY, IT, RN>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else
                 merge_chain_blk<KEY, IT, CH == 2>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
@@ -1130,8 +1218,17 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
             // a lane's outputs past its pair's end are MAX (the chain ran into
             // the sentinels), the value the sentinel stores write there too
             if (pos < Q + LP) {
+                if constexpr (CH == 3) {
+                    // output j is r[ex + j]: one store per key from base pos - ex
+                    KEY* q = s + pos - ex;
 #pragma unroll
-                for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
+                    for (int k = 0; k < RN; ++k)
+                        if (k >= ex && k < ex + IT) q[k] = r[k];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < IT; j += 2)
+                        *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
+                }
             }
             for (int x = tid; x < P * G; x += NT) {
                 const int p = x / G;
@@ -1154,9 +1251,10 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 2
     // land past the chunk)
     const int sh = (int)(out0 & (VK - 1));
     if (pos < len) {
-        KEY* q = s + sh + pos;
+        KEY* q = s + sh + pos - ex;
 #pragma unroll
-        for (int j = 0; j < IT; ++j) q[j] = r[j];
+        for (int k = 0; k < RN; ++k)
+            if (k >= ex && k < ex + IT) q[k] = r[k];
     }
     __syncthreads();
     const int nv = (sh + len + VK - 1) / VK;

@@ -242,7 +242,7 @@ def _multiset_props64(t):
 
 
 def test_past_the_multiway_limit_u32(ctx):
-    """2^31 - 3 u32 keys: five 8-way passes end at runs of 2^30 (32-bit row
+    """2^31 - 3 u32 keys: four multi-way passes end at runs of 2^30 (32-bit row
     offsets), one 2-way pass merges the last level; ragged tail."""
     n = (1 << 31) - 3
     plan = misort.plan(n, 4)

@@ -195,7 +195,8 @@ ctx.close()
     (4, {"MISORT_RUN_NT": "1024"}, (1 << 22) + 8191),
     (4, {"MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),
     (4, {"MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
-    (4, {}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
+    (4, {"MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
+    (4, {}, (1 << 27) + 777),  # the default: three 16-way passes
     (4, {}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
     (4, {"MISORT_MULTIWAY": "4"}, (1 << 25) + 3),  # 4 + 3 + 3 levels (16-way)
     (4, {}, 3 * (1 << 23) + 5),
@@ -228,8 +229,8 @@ def test_full_sort_merge_passes(kb, env, n):
     line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
     _, count, _, countk, verdict = line.split()
     assert verdict == "OK", line
-    if kb == 4:  # default: 8-way passes when the levels split into threes, else up to 16-way
-        cap = int(env["MISORT_MULTIWAY"]) if "MISORT_MULTIWAY" in env else (3 if int(count) % 3 == 0 else 4)
+    if kb == 4:  # default: the fewest passes of up to 16-way
+        cap = int(env["MISORT_MULTIWAY"]) if "MISORT_MULTIWAY" in env else 4
     else:
         cap = int(env.get("MISORT_MULTIWAY_U64", "4"))
     if cap >= 2 and int(count) >= 2:

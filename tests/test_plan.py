@@ -67,23 +67,24 @@ def test_plan_covers_the_levels(n, key_bytes):
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + five 8-way passes (levels 16..30, three per pass; one
-    # 2-way merge pass per level would be 1 + 15)
+    # 2^30 u32: 1 SORT + four multi-way passes (levels 16..30: three 16-way
+    # and one 8-way; one 2-way merge pass per level would be 1 + 15)
     p30 = misort.plan(1 << 30, 4)
     assert p30[0][0] == KIND_SORT
-    assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 15 + 3 * i, 3) for i in range(5)]
-    # 13 and 14 levels: four passes, one or two of them 16-way (fewer passes win
-    # unless the levels split into 8-way passes exactly); 12 levels: four 8-way
+    assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 15, 4), (KIND_RUNSK, 19, 4), (KIND_RUNSK, 23, 4),
+                                                (KIND_RUNSK, 27, 3)]
+    # the fewest passes of at most four levels (16-way) at every size
+    # (profiles/r04/mw: faster than 8-way passes from 2^26 to 2^31)
     assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [4, 3, 3, 3]
     assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [4, 4, 3, 3]
-    assert [q[2] for q in misort.plan(1 << 27, 4)[1:]] == [3, 3, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 27, 4)[1:]] == [4, 4, 4]
     assert [q[2] for q in misort.plan(1 << 25, 4)[1:]] == [4, 3, 3]
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
-    assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 5 + [KIND_RUNS]
+    assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 4 + [KIND_RUNS]
     # small u32 sorts take the merge passes too (round 3: they beat the bitonic
     # network's ROWS/SPAN/MERGE passes at every size, profiles/r03/small_u32)
     assert [q[0] for q in misort.plan(1 << 23, 4)] == [KIND_SORT] + [KIND_RUNSK] * 2  # 4 + 4 levels
-    assert [q[0] for q in misort.plan(1 << 24, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^24: 3 x 8-way
+    assert [q[0] for q in misort.plan(1 << 24, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^24: 3 x 8-way (9 levels)
     assert [q[0] for q in misort.plan(1 << 16, 4)] == [KIND_SORT, KIND_RUNS]  # one level: 2-way
     assert [q[0] for q in misort.plan(1 << 15, 4)] == [KIND_SORT]  # one tile
     # u64: 2^13-key SORT tiles, then 16 levels in four 16-way passes

@@ -39,5 +39,17 @@ for cn, key in (("FETCH_SIZE", "read"), ("WRITE_SIZE", "write")):
         e[f"{cn.lower()}_bytes"] = v * 1024
         known = sh[f"{key}_bytes"]
         e[f"{key}_scale"] = known / (v * 1024) if known > 0 and v > 0 else None
+# probe4 reads 4 B per distinct 128-B line: its counter bytes per probe show
+# the granule one scattered dword costs (not a counter error); for traffic a
+# probe's counter bytes are scaled like the line reads'
+pr = out["shapes"].get("probe4")
+if pr and pr.get("fetch_size_bytes"):
+    nprobe = pr["read_bytes"] / 4
+    pr["counter_bytes_per_probe"] = pr["fetch_size_bytes"] / nprobe
+    pr["read_scale_algorithmic"] = pr["read_scale"]
+    pr["read_scale"] = out["shapes"]["line128"]["read_scale"]
+    pr["note"] = ("a scattered 4-B read is counted as one 64-B request (counter bytes per probe), a 128-B "
+                  "line by the x2 rule of the streaming shapes; "
+                  "read_scale = line128's, read_scale_algorithmic = 4 B / counter bytes")
 json.dump(out, sys.stdout, indent=1)
 print()

@@ -39,11 +39,14 @@ def u64_mix(n, seed):
     g = torch.Generator(device="cuda")
     g.manual_seed(seed)
     kind = torch.rand(n, generator=g, device="cuda")
-    alpha = torch.randint(-2**63, 2**63 - 1, (1024,), generator=g, device="cuda", dtype=torch.int64)
+    def bits(m, hi_bits):  # m random int64 of hi_bits + 32 bits
+        hi = torch.randint(0, 1 << hi_bits, (m,), generator=g, device="cuda", dtype=torch.int64)
+        return (hi << 32) | torch.randint(0, 1 << 32, (m,), generator=g, device="cuda", dtype=torch.int64)
+    alpha = bits(1024, 32)  # full 64-bit patterns (int64 wraps: u64 keys)
     x = alpha[torch.randint(0, 1024, (n,), generator=g, device="cuda")]
     u = torch.rand(n, generator=g, device="cuda", dtype=torch.float64)
     odd = (u * u).view(torch.int64)
-    uni = torch.randint(0, 2**63 - 1, (n,), generator=g, device="cuda", dtype=torch.int64)
+    uni = bits(n, 31)  # uniform < 2^63
     x = torch.where(kind >= 0.4, odd, x)
     x = torch.where(kind >= 0.7, uni, x)
     x = torch.where(kind >= 0.9, torch.zeros_like(x), x)
@@ -68,14 +71,17 @@ def main():
     p = a.p
     sizes = misort.block_sizes(n, p)
     ctx = misort.Context(0)
-    s = torch.cuda.current_stream()
+    # one non-default stream for torch and misort alike: misort takes the
+    # current torch stream (stream=None), but maps the null stream to its own
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
     kb = 4 if a.dtype == "u32" else 8
     npdt = np.uint32 if kb == 4 else np.uint64
     blocks = []
     if kb == 4:
         for r in range(p):
             b = torch.empty(sizes[r], dtype=torch.int32, device="cuda")  # int32 storage = u32 keys
-            ctx.fill_splitmix(b, 0x5EED0003, sum(sizes[:r]), stream=s)
+            ctx.fill_splitmix(b, 0x5EED0003, sum(sizes[:r]))
             blocks.append(b)
     else:
         allk = u64_mix(n, 0x5EED0005)
@@ -85,7 +91,7 @@ def main():
     # emulate the schedule, one rank after another (whole-block compare-splits)
     for r in range(p):
         out = torch.empty_like(blocks[r])
-        ctx.local_sort(blocks[r], out, stream=s)
+        ctx.local_sort(blocks[r], out)
         blocks[r] = out
     sched = [misort.schedule(p, r) for r in range(p)]
     stages = []
@@ -104,10 +110,10 @@ def main():
         new = []
         for r in range(p):
             pr, kp = sched[r][st]
-            new.append(ctx.compare_split(blocks[r], blocks[pr], kp, stream=s))
+            new.append(ctx.compare_split(blocks[r], blocks[pr], kp))
         blocks = new
     torch.cuda.synchronize()
-    errs = sum(ctx.check_sort(b, stream=s) for b in blocks)
+    errs = sum(ctx.check_sort(b) for b in blocks)
     del blocks
     torch.cuda.empty_cache()
 
@@ -130,7 +136,7 @@ def main():
     res = {"n_total": n, "p": p, "dtype": a.dtype, "rank": 0, "n_rank": sizes[0], "reps": a.reps,
            "check_errors": int(errs)}
     out0 = torch.empty_like(first)
-    t = timed(lambda: ctx.local_sort(first, out0, stream=s))
+    t = timed(lambda: ctx.local_sort(first, out0))
     res["local_sort"] = {"ms": t, "keys": sizes[0], "passes": [x[0] for x in misort.plan(sizes[0], kb)]}
     rows = []
     for x in stages:
@@ -142,7 +148,7 @@ def main():
             row.update(encode_ms=enc_ms, decode_ms=dec_ms, coded_bytes=nbytes, raw_bytes=k * w,
                        codec_ok=bool(torch.equal(dec, x["recv"])))
             mo = torch.empty_like(x["mine"])
-            t = timed(lambda: ctx.compare_split(x["mine"], x["recv"], x["keep_max"], out=mo, stream=s))
+            t = timed(lambda: ctx.compare_split(x["mine"], x["recv"], x["keep_max"], out=mo))
             # merge-split bytes: read n_me + k, write n_me
             mb = (2 * x["n_me"] + k) * w
             row.update(merge_split_ms=t, merge_split_bytes=mb, merge_split_TBs=mb / (t * 1e-3) / 1e12,

@@ -27,7 +27,8 @@ acc = collections.defaultdict(list)
 for s, e, name in rows[cut + 1:]:
     if "misort" not in name:
         continue
-    key = re.sub(r"\(.*", "", name).replace("void misort::(anonymous namespace)::", "").replace("misort::", "")
+    key = name.replace("misort::(anonymous namespace)::", "").replace("misort::", "").replace("void ", "")
+    key = re.sub(r"\(.*", "", key)
     acc[key].append((e - s) / 1e3)
 print(f"# {os.path.basename(os.path.normpath(root))}: {sum(len(v) for v in acc.values())} misort dispatches "
       f"after the marker (dispatch {cut})")
