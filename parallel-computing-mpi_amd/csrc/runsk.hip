@@ -104,6 +104,20 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_SORT_LT_U32
 #define MISORT_SORT_LT_U32 15  // the u32 SORT tile (bitonic.h)
 #endif
+// 16-way u32 passes: larger chunks.  A chunk holds FM * FG = CAP - K * FG
+// keys on average, so at K = 16 a quarter of an 8192-key chunk's lanes idle;
+// 22 outputs per lane (CAP 10752, three workgroups per CU) measured 2^30
+// 68.9 -> 69.8 Gkeys/s, 2^28 +0.4 %, 2^27 +-0 (profiles/r04/chunk16); 24 per
+// lane (CAP 11776) was 12 % slower.  0 = the 8-way shape for every pass.
+#ifndef MISORT_MK_IT16
+#define MISORT_MK_IT16 22
+#endif
+#ifndef MISORT_MK_CAP16
+#define MISORT_MK_CAP16 10752
+#endif
+#ifndef MISORT_MK_WGCU16
+#define MISORT_MK_WGCU16 3
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -111,6 +125,11 @@ struct KTr<uint32_t> {
     static constexpr int IT = MISORT_MK_IT ? MISORT_MK_IT : NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
     static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
+    // the chunk shape of a pass of lk levels
+    static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
+    static constexpr int it(int lk) { return big(lk) ? MISORT_MK_IT16 : IT; }
+    static constexpr int cap(int lk) { return big(lk) ? MISORT_MK_CAP16 : CAP; }
+    static constexpr int wg(int lk) { return big(lk) ? MISORT_MK_WGCU16 : WG_PER_CU; }
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = MISORT_SORT_LT_U32 < 15 ? MISORT_SORT_LT_U32 : 15, LWK_MAX = 30;  // runs >= the SORT tile; 32-bit row offsets
 };
@@ -126,6 +145,9 @@ struct KTr<uint64_t> {
     static constexpr int WG_PER_CU = 2;
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
+    static constexpr int it(int) { return IT; }
+    static constexpr int cap(int) { return CAP; }
+    static constexpr int wg(int) { return WG_PER_CU; }
 };
 template <typename KEY>
 constexpr KEY KMAX = (KEY)~(KEY)0;
@@ -144,7 +166,7 @@ struct Shape {
     // the merge chain of the in-LDS levels (MISORT_MK_CHAIN*) and the sentinels
     // after each sequence: G >= the keys a chain may read past its sequence
     static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
-    static constexpr int NT = T::NT, IT = T::IT, CAP = T::CAP;
+    static constexpr int NT = T::NT, IT = T::it(LK), CAP = T::cap(LK);
     // chain 3 merges RN = IT + 2 keys rounded up to even (the lane's IT outputs
     // after up to two early keys) and reads up to RN + 2 - 2 keys past a
     // sequence start; chains 0-2 read up to IT
@@ -161,7 +183,10 @@ struct Shape {
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
     static constexpr int RW = LK == 4 ? 64 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
-    static constexpr int LS = (T::IT + 1) & ~1;    // load slots per lane (18 at IT = 17 or 18)
+    // load slots per lane: enough rows for CAP keys in K segments (18 at
+    // CAP = 8192, IT = 17 or 18)
+    static constexpr int LS_ROWS = ((CAP + RW - 1) / RW + K + NR - 1) / NR;
+    static constexpr int LS = ((IT + 1) & ~1) > LS_ROWS ? ((IT + 1) & ~1) : LS_ROWS;
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_KEYS = PAD + CAP + K * (G + QA) + 16;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
@@ -233,7 +258,7 @@ struct Geo {
 
 template <typename KEY>
 Geo make_geo(int64_t n, int lw, int lk) {
-    Geo geo{n, lw, lk, KTr<KEY>::CAP / (int)FG - (1 << lk), 0, 0};
+    Geo geo{n, lw, lk, KTr<KEY>::cap(lk) / (int)FG - (1 << lk), 0, 0};
     geo.nfull = n >> (lw + lk);
     geo.kf = ((((int64_t)1 << (lw + lk)) >> FG_LOG2) + geo.fm - 1) / geo.fm;
     return geo;
@@ -884,8 +909,10 @@ template <typename KEY>
 __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
     // first co-rank step: the largest power of two <= CAP/2 (hi - lo <= CAP/2;
     // the steps must be powers of two for the lifting search)
-    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(KTr<KEY>::CAP / 2)));
-    static_assert(KTr<KEY>::CAP / 2 <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
+    // (from the largest chunk of any pass: steps above maxr are skipped)
+    constexpr int CMAX = KTr<KEY>::cap(4) > KTr<KEY>::CAP ? KTr<KEY>::cap(4) : KTr<KEY>::CAP;
+    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(CMAX / 2)));
+    static_assert(CMAX / 2 <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
     const KEY* a = s + A0 - 1;
@@ -902,34 +929,6 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     return base;
 }
 
-// co_rank at diagonal d, searched from diagonal d + 1 by the lanes 16..31 of
-// each 32-lane LDS group (MISORT_MK_SKEW): with IT even the lanes' diagonals
-// (IT apart) fall on only 16 of the 32 banks, so every search step that the
-// lanes take at a common base is a 2-way conflict on its B probe (and on its
-// A probe where the bases are d - LB); the one-off skew puts the 32 probes on
-// 32 banks.  The split at d is the split at d + 1 less its larger last key
-// (the d-th output): two more reads for the skewed lanes.
-#ifndef MISORT_MK_SKEW
-#define MISORT_MK_SKEW 1
-#endif
-template <typename KEY>
-__device__ __forceinline__ int co_rank_skew(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
-    if constexpr (!MISORT_MK_SKEW) {
-        return co_rank<KEY>(s, A0, LA, B0, LB, d, maxr);
-    } else {
-        const bool sk = (__lane_id() & 16) && d < LA + LB;
-        const int dq = d + (sk ? 1 : 0);
-        const int iq = co_rank<KEY>(s, A0, LA, B0, LB, dq, maxr);
-        if (!sk) return iq;
-        // the d-th output is max(A[iq - 1], B[dq - iq - 1]) (a side with no key
-        // before the split cannot give it)
-        const int jq = dq - iq;
-        const KEY a = s[A0 + iq - 1], b = s[B0 + jq - 1];
-        const bool fromA = jq == 0 || (iq > 0 && a > b);
-        return fromA ? iq - 1 : iq;
-    }
-}
-
 // IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
 // both followed by sentinels.  A chain holds h, the head of the side it took
 // last, and g, the other side's head: each step outputs min(h, g), keeps
@@ -943,7 +942,7 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
                                             KEY (&r)[IT]) {
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
-    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
     // byte addresses of the two heads (LDS pointers are 32-bit)
     uint32_t px = lds_addr<KEY>(s + A0 + ia), py = lds_addr<KEY>(s + B0 + dc - ia);
     KEY h = lds_ld<KEY>(px), g = lds_ld<KEY>(py);
@@ -1028,7 +1027,7 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     static_assert(IT % 2 == 0, "two outputs per step");
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;
-    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
     constexpr uint32_t B2 = 2 * sizeof(KEY);
     const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
     const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
@@ -1065,7 +1064,7 @@ __device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int 
     static_assert(RN % 2 == 0 && RN >= IT + 2, "two outputs per step, two early keys");
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;
-    const int ia = co_rank_skew<KEY>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr);
     const int ib = dc - ia;
     constexpr uint32_t B2 = 2 * sizeof(KEY);
     const uint32_t pa = lds_addr<KEY>(s + A0 + (ia & ~1)), pb = lds_addr<KEY>(s + B0 + (ib & ~1));
@@ -1098,7 +1097,7 @@ __device__ __forceinline__ int row_part(int tid) {
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
 template <typename KEY, int LK, bool FENCES, int MODE = 0>
-__global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::WG_PER_CU* KTr<KEY>::NT / 256) void k_mergek(
+__global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256) void k_mergek(
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
