@@ -902,29 +902,52 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
 // split gives the same output values -- the keys carry no payload).  The
 // largest base in [lo, hi] with A[i - 1] <= B[d - i] for every i <= base, by
 // power-of-two steps with clamped probes, no data-dependent branches: the
-// steps 2^j <= maxr, a uniform bound on hi - lo <= min(LA, LB) (<= CAP/2 =
-// 2^12), sum to >= hi - lo.  Probe addresses stay inside [A0 - 1, A0 + LA)
+// steps 2^j <= maxr + PH, a uniform bound on hi - lo (<= min(LA, LB)) plus the
+// phase, sum to >= hi - lo + PH.  Probe addresses stay inside [A0 - 1, A0 + LA)
 // and [B0, B0 + LB].
+//
+// Phase (MISORT_MK_PHASE): lane l of each 32-lane LDS group starts its search
+// at lo - (l % 32) (positions <= lo count as true: the answer is >= lo).  With
+// a common start, lanes whose bases differ at a coarse step differ by a
+// multiple of 2 * step, so their A probes land in ONE bank (step >= 16): the
+// searches were k_mergek's largest LDS cost (SQ probe modes,
+// profiles/r04/sq_attr: 5 conflict cycles per probe instruction, more wave
+// cycles than the merge chains).  The phases put those probes on distinct
+// banks, and the B probes at (IT + 1) * l on distinct banks too.  Measured
+// on one box (profiles/r04/phase): u32 k_mergek 2524 -> 2435 us per 2^30
+// pass, 571 -> 545 at 2^28 (SQ: 3.1 -> 1.6 conflict cycles per search probe);
+// u64 (two-bank keys, 4 waves per SIMD) 2667 -> 2739 us, so u64 keeps a
+// common start.
+#ifndef MISORT_MK_PHASE
+#define MISORT_MK_PHASE 1
+#endif
 template <typename KEY>
 __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
-    // first co-rank step: the largest power of two <= CAP/2 (hi - lo <= CAP/2;
-    // the steps must be powers of two for the lifting search)
-    // (from the largest chunk of any pass: steps above maxr are skipped)
+    // first co-rank step: the largest power of two <= CAP/2 + PH (hi - lo <=
+    // CAP/2; the steps must be powers of two for the lifting search), from the
+    // largest chunk of any pass: steps above maxr + PH are skipped
+    constexpr int PH = MISORT_MK_PHASE && sizeof(KEY) == 4 ? 31 : 0;
     constexpr int CMAX = KTr<KEY>::cap(4) > KTr<KEY>::CAP ? KTr<KEY>::cap(4) : KTr<KEY>::CAP;
-    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(CMAX / 2)));
-    static_assert(CMAX / 2 <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
+    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(CMAX / 2 + PH)));
+    static_assert(CMAX / 2 + PH <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
     const int lo = d - LB > 0 ? d - LB : 0;
     const int hi = d < LA ? d : LA;
     const KEY* a = s + A0 - 1;
     const KEY* b = s + B0 + d;
-    int base = lo;
+    int base = lo - (PH ? (int)(__lane_id() & 31) : 0);
 #pragma unroll
     for (int step = CO_STEP0; step >= 1; step >>= 1) {
-        if (step > maxr) continue;  // uniform
+        if (step > maxr + PH) continue;  // uniform
         const int i = base + step;
-        const int ic = i < hi ? i : hi;
-        const bool ok = i <= hi && a[ic] <= b[-ic];
-        base = ok ? i : base;
+        if constexpr (PH) {
+            const int ic = i < lo ? lo : (i < hi ? i : hi);  // v_med3_i32
+            const bool ok = i <= lo || (i <= hi && a[ic] <= b[-ic]);
+            base = ok ? i : base;
+        } else {
+            const int ic = i < hi ? i : hi;
+            const bool ok = i <= hi && a[ic] <= b[-ic];
+            base = ok ? i : base;
+        }
     }
     return base;
 }
@@ -1093,7 +1116,9 @@ __device__ __forceinline__ int row_part(int tid) {
 }
 
 // k_mergek: one workgroup per chunk.  MODE (probes only, MISORT_MK_PROBE):
-// 0 = the pass; 1 = no merge (the access pattern's floor); 2 = level 1 only.
+// 0 = the pass; 1 = no merge (the access pattern's floor); 2 = level 1 only;
+// 3 = the co-rank searches of every level without the chains (for SQ
+// attribution: 3 - 1 = the searches, 0 - 3 = the chains).
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
 template <typename KEY, int LK, bool FENCES, int MODE = 0>
@@ -1200,10 +1225,14 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
             LP = in ? lp[p] : LP;
         }
         const int end = qp[P - 1] + lp[P - 1];
-        if (MODE == 1 || (MODE == 2 && lv > 1)) {
+        if (MODE == 1 || (MODE == 2 && lv > 1) || MODE == 3) {
             ex = 0;
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
+            if (MODE == 3 && wpos < end) {  // the search alone, its result kept alive
+                const int dc = pos - Q < LA + LB ? pos - Q : LA + LB;
+                r[0] ^= (KEY)(co_rank<KEY>(s, A0, LA, B0, LB, dc, maxr) & 1);
+            }
         } else if (wpos < end) {
             if constexpr (CH == 0)
                 merge_chain<KEY, IT>(s, A0, LA, B0, LB, pos - Q, maxr, r);
@@ -1472,6 +1501,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         }
         k_mergek<KEY, LK, false, 1><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
         k_mergek<KEY, LK, false, 2><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+        k_mergek<KEY, LK, false, 3><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
     }
     return hipGetLastError();
 }
