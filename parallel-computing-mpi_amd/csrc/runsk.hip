@@ -921,6 +921,11 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
 #ifndef MISORT_MK_PHASE
 #define MISORT_MK_PHASE 1
 #endif
+// 2: clamped probes, one compare per step (co_rank); 1: the range checks as
+// exec-mask branches (round 3)
+#ifndef MISORT_MK_COR
+#define MISORT_MK_COR 2
+#endif
 template <typename KEY>
 __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
     // first co-rank step: the largest power of two <= CAP/2 + PH (hi - lo <=
@@ -935,6 +940,24 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     const KEY* a = s + A0 - 1;
     const KEY* b = s + B0 + d;
     int base = lo - (PH ? (int)(__lane_id() & 31) : 0);
+    if constexpr (MISORT_MK_COR == 2) {
+        // every probe clamped into [lo, hi], both loads unconditional: a
+        // probe at hi that holds makes hi the answer (later probes repeat
+        // it); a step that ends below lo tests lo, which holds by definition
+        // (the answer is >= lo) and moves base up to lo, within the steps
+        // left.  No exec-mask branches; with a common start (PH = 0) no step
+        // ends below lo.
+#pragma unroll
+        for (int step = CO_STEP0; step >= 1; step >>= 1) {
+            if (step > maxr + PH) continue;  // uniform
+            const int t = base + step;
+            int i;  // clamp(t, lo, hi) (the compiler emits min + cmp + cndmask)
+            asm("v_med3_i32 %0, %1, %2, %3" : "=v"(i) : "v"(t), "v"(lo), "v"(hi));
+            const bool ok = (PH != 0 && i == lo) | (a[i] <= b[-i]);
+            base = ok ? i : base;
+        }
+        return base > lo ? base : lo;
+    }
 #pragma unroll
     for (int step = CO_STEP0; step >= 1; step >>= 1) {
         if (step > maxr + PH) continue;  // uniform
