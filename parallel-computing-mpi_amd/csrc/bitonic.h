@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "lds_merge.h"
 
 namespace misort {
 
@@ -65,6 +66,8 @@ struct PlanKnobs {
     // 2^24 +8 %, 2^26 +4 %, 2^27 +1.5 %, 2^29 +2.5 % over 8-way): fewer
     // passes, and u64 chains cost less per byte than u32 ones
     int multiway_u64 = 4;
+    // u32 SORT tile (log2 keys): 0 (default) = per size (sort_tile_u32), 14 or 15 = always
+    int sort_tile_u32 = 0;
     PlanKnobs();
     // the cap for L levels
     int multiway_cap(int kb, int L) const {
@@ -81,16 +84,11 @@ namespace {
 
 template <typename K>
 struct KT;
-// Probe-only (tools/build_variant.sh): log2 keys of the u32 SORT tile (14: 512
-// lanes, 64 KiB + padding, two workgroups per CU).
-#ifndef MISORT_SORT_LT_U32
-#define MISORT_SORT_LT_U32 15
-#endif
 template <>
 struct KT<uint32_t> {
     static constexpr uint32_t MAX = 0xFFFFFFFFu;
     static constexpr int V = 4;   // keys per 16-byte vector
-    static constexpr int LT = MISORT_SORT_LT_U32; // log2 keys per SORT tile (15: 128 KiB + padding)
+    static constexpr int LT = SORT_LT_U32;  // log2 keys of the larger SORT tile (kernels.h)
     typedef uint32_t vec __attribute__((ext_vector_type(4)));
 };
 template <>
@@ -590,9 +588,8 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
 // next tile's prefetch issued an s_waitcnt vmcnt(0) that waited for the whole
 // prefetch (vmcnt is in order), so the prefetch hid nothing.  The tile base is
 // uniform (SGPRs); lanes add 32-bit offsets.
-template <bool FULL>
+template <int LT, bool FULL>
 __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* in, int64_t tile, int64_t n, int t) {
-    constexpr int LT = KT<uint32_t>::LT;
     const uint32_t* tb = in + (tile << LT);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -607,22 +604,76 @@ __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* i
     }
 }
 
-constexpr int SORT_U32_NT = TileGeo<uint32_t, KT<uint32_t>::LT>::NT;
-constexpr int SORT_U32_WPE = KT<uint32_t>::LT == 15 ? 1 : TileGeo<uint32_t, KT<uint32_t>::LT>::WAVES_PER_EU;
-template <bool PERSIST, bool FULL>
-__global__ __launch_bounds__(SORT_U32_NT, SORT_U32_WPE) void k_sort_u32(const uint32_t* in, uint32_t* out, int64_t n,
-                                                                        int64_t ntiles, int64_t tile0, uint64_t* fence,
-                                                                        int flk) {
+// The u32 SORT tile's top levels as merge levels (MISORT_SORT_MERGE = 12):
+// levels 1..11 run as the bitonic network (registers, DPP, wave-local LDS
+// phases: each wave then holds a sorted run of 2^11 keys), then the 16 runs
+// are laid out plainly in LDS with sentinels after each and merged pairwise in
+// four levels by the multi-way pass's in-LDS machinery (lds_merge.h: phased
+// co-rank searches, two-key chains), 33 outputs per lane -- instead of levels
+// 12..LT as barrier-separated LDS phases (1.83 of the 2^15 pass's 4.8 ms).
+// The merge keeps 34 more registers per lane live than the network, so the
+// tile runs one workgroup per tile (no next-tile prefetch in registers: it
+// would spill); with MISORT_SORT_LT_U32 = 14 two workgroups per CU overlap
+// each other's loads.  0 = the bitonic network for every level.
+#ifndef MISORT_SORT_MERGE
+#define MISORT_SORT_MERGE 12
+#endif
+template <int LT>
+struct SortMergeShape {
+    static constexpr int K = 1 << (LT - 11), LKS = LT - 11, NT = 1 << (LT - 5);  // 2^11-key runs, 32 keys per lane
+    static constexpr int IT = 33;       // odd: lanes' diagonals on distinct banks; NT x 33 >= 2^LT + pair gaps
+    static constexpr int RN = IT + 1;   // the two-key chain merges an even count
+    static constexpr int G = RN + 1;    // sentinels after each sequence (a chain reads <= RN past it)
+    static constexpr int QA = IT;       // pairs start at lane boundaries
+    static constexpr int CH = 1;
+    static constexpr int MAXR = 1 << (LT - 1);  // a last-level pair: two runs of 2^(LT-1)
+    static constexpr int RUN = 1 << 11, GS = G;
+    static constexpr int WORDS = NT * IT + G + 8;  // the level layouts (>= K runs of RUN + GS)
+    static_assert(K * (RUN + GS) <= WORDS && (1 << LT) + (K / 2) * (G + QA) <= NT * IT, "SORT merge layout");
+};
+
+// LDS (plain layout) -> 16-byte vectors -> HBM, and the first multi-way
+// pass's fences (final_store for the merge-level tile).
+template <int LT>
+__device__ __forceinline__ void final_store_plain(const uint32_t* s, uint32_t* out, int64_t tile, int64_t n, bool full,
+                                                  int t, uint64_t* fence, int flk) {
+    typedef TileGeo<uint32_t, LT> G;
+#pragma unroll
+    for (int k = 0; k < G::LOADS; ++k) {
+        const int e = place<uint32_t, LT>(k, t);
+        const KT<uint32_t>::vec v = *reinterpret_cast<const KT<uint32_t>::vec*>(s + e);
+        uint32_t x[4] = {v[0], v[1], v[2], v[3]};
+        store_slot<uint32_t, LT>(out, tile, n, full, e, x);
+        constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
+        const int64_t gi = (tile << LT) + e;
+        if (fence && (e & FGM) == 0 && gi < n) {
+            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
+                                 (uint32_t)(e >> MERGEK_FENCE_LOG2);
+            fence[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
+        }
+    }
+}
+
+// 2^15 tile: 1024 lanes, one workgroup per CU; 2^14: 512 lanes, two
+// workgroups per CU (4 waves per SIMD: 128 VGPRs per lane)
+template <int LT, bool PERSIST, bool FULL>
+__global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
+    const uint32_t* in, uint32_t* out, int64_t n, int64_t ntiles, int64_t tile0, uint64_t* fence, int flk) {
     typedef uint32_t K;
-    constexpr int LT = KT<uint32_t>::LT;
     typedef TileGeo<K, LT> G;
+    static_assert(LT == 14 || LT == 15, "u32 SORT tiles");
     constexpr int WL = MISORT_WAVE_LEVELS;
     static_assert(G::LOADS == 8 && (G::NT == 1024 || G::NT == 512) && WL >= 5 && WL <= 10, "u32 SORT tile shape");
-    __shared__ K s[lds_words(G::T)];
+    constexpr bool MERGE = MISORT_SORT_MERGE == 12 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
+    typedef SortMergeShape<LT> MS;
+    // MERGE: 4 words below the tile (a co-rank probe may read index -1)
+    __shared__ __attribute__((aligned(16))) K sbuf[(MERGE ? (MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T)) + 4
+                                                          : lds_words(G::T))];
+    K* s = MERGE ? sbuf + 4 : sbuf;
     int64_t tile = tile0 + blockIdx.x;
     if (tile >= ntiles) return;
     K pre[G::LOADS][G::V];
-    sort_fetch<FULL>(pre, in, tile, n, (int)threadIdx.x);
+    sort_fetch<LT, FULL>(pre, in, tile, n, (int)threadIdx.x);
     for (; tile < ntiles; tile += gridDim.x) {
         // lane id through an opaque copy: the per-lane LDS/HBM addresses are
         // recomputed every tile instead of being hoisted into ~16 loop-invariant
@@ -656,9 +707,43 @@ __global__ __launch_bounds__(SORT_U32_NT, SORT_U32_WPE) void k_sort_u32(const ui
         // before the wave levels, so their registers and the cross-lane
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
-        if (PERSIST && nxt < ntiles) sort_fetch<FULL>(pre, in, nxt, n, t);
-        sort_levels_w<K, WL + 1, (MISORT_SORT_TOP < LT ? MISORT_SORT_TOP : LT)>(s, t);
-        final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
+        if (PERSIST && nxt < ntiles) sort_fetch<LT, FULL>(pre, in, nxt, n, t);
+        if constexpr (MERGE) {
+            sort_levels_w<K, WL + 1, 11>(s, t);
+            // wave w's sorted run (keys w * 2^11 ...) -> plain layout at
+            // w * (RUN + GS), then GS sentinels; lane l moves keys 64c + l
+            // (consecutive lanes, consecutive words: no bank conflicts)
+            const int w = t >> 6, l = t & 63;
+            uint32_t y[32];
+#pragma unroll
+            for (int c = 0; c < 32; ++c) y[c] = s[pad((w << 11) + (c << 6) + l)];
+            __syncthreads();
+            const int b0 = w * (MS::RUN + MS::GS);
+#pragma unroll
+            for (int c = 0; c < 32; ++c) s[b0 + (c << 6) + l] = y[c];
+            if (l < MS::GS) s[b0 + MS::RUN + l] = 0xFFFFFFFFu;
+            __syncthreads();
+            int st[MS::K], ln[MS::K];
+#pragma unroll
+            for (int q = 0; q < MS::K; ++q) {
+                st[q] = q * (MS::RUN + MS::GS);
+                ln[q] = MS::RUN;
+            }
+            uint32_t r[MS::RN];
+            int ex = 0;
+            lds_merge_levels<uint32_t, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
+            // the merged tile: lane t's outputs [33 t, 33 t + 33) back to LDS
+            // (the last level's reads are done), then out as 16-byte vectors
+            if (t * MS::IT < G::T) {
+#pragma unroll
+                for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
+            }
+            __syncthreads();
+            final_store_plain<LT>(s, out, tile, n, FULL, t, fence, flk);
+        } else {
+            sort_levels_w<K, WL + 1, (MISORT_SORT_TOP < LT ? MISORT_SORT_TOP : LT)>(s, t);
+            final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
+        }
         if constexpr (!PERSIST) break;
         __syncthreads();
     }
@@ -666,32 +751,38 @@ __global__ __launch_bounds__(SORT_U32_NT, SORT_U32_WPE) void k_sort_u32(const ui
 
 // fence/flk: see final_store (null: no fences).
 // ea/eb: timing events carried by the first / last launch (null: none).
-inline void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
-                            int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
+template <int LT>
+void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
+                     int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
+    constexpr int NT = TileGeo<uint32_t, LT>::NT;
+    // the merge-level tile runs one workgroup per tile (see MISORT_SORT_MERGE)
+    constexpr bool MERGE = MISORT_SORT_MERGE == 12 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
     static int64_t cap = 0;
-    const int64_t nfull = n >> KT<uint32_t>::LT;
-    const bool persist = plan_knobs().persist_sort(4);
-    if (persist && cap == 0) {
-        int per_cu = 0, cus = 0, dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<true, true>, SORT_U32_NT, 0);
-        cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
-    }
-    const bool tail = (nfull << KT<uint32_t>::LT) < n;
+    const int64_t nfull = n >> LT;
+    const bool persist = !MERGE && plan_knobs().persist_sort(4);
+    const bool tail = (nfull << LT) < n;
     if (nfull > 0) {
-        const int64_t want = persist ? cap * plan_knobs().grid_mult : nfull;
-        const int64_t grid = nfull < want ? nfull : want;
         hipEvent_t b = tail ? nullptr : eb;
-        if (persist)
-            launch_timed(k_sort_u32<true, true>, dim3((unsigned)grid), dim3(SORT_U32_NT), 0, s, ea, b, in, out, n, nfull,
-                         (int64_t)0, fence, flk);
-        else
-            launch_timed(k_sort_u32<false, true>, dim3((unsigned)grid), dim3(SORT_U32_NT), 0, s, ea, b, in, out, n, nfull,
+        if constexpr (!MERGE) {
+            if (persist) {
+                if (cap == 0) {
+                    int per_cu = 0, cus = 0, dev = 0;
+                    (void)hipGetDevice(&dev);
+                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sort_u32<LT, true, true>, NT, 0);
+                    cap = (int64_t)(per_cu < 1 ? 1 : per_cu) * (cus < 1 ? 1 : cus);
+                }
+                const int64_t want = cap * plan_knobs().grid_mult;
+                launch_timed(k_sort_u32<LT, true, true>, dim3((unsigned)(nfull < want ? nfull : want)), dim3(NT), 0, s,
+                             ea, b, in, out, n, nfull, (int64_t)0, fence, flk);
+            }
+        }
+        if (!persist)
+            launch_timed(k_sort_u32<LT, false, true>, dim3((unsigned)nfull), dim3(NT), 0, s, ea, b, in, out, n, nfull,
                          (int64_t)0, fence, flk);
     }
     if (tail)
-        launch_timed(k_sort_u32<false, false>, dim3(1), dim3(SORT_U32_NT), 0, s, nfull > 0 ? nullptr : ea, eb, in, out, n,
+        launch_timed(k_sort_u32<LT, false, false>, dim3(1), dim3(NT), 0, s, nfull > 0 ? nullptr : ea, eb, in, out, n,
                      nfull + 1, nfull, fence, flk);
 }
 
@@ -730,6 +821,20 @@ inline std::vector<Pass> plan_uncached(int k, int key_bytes, int LT) {
     return ps;
 }
 
+// The u32 SORT tile for 2^k-key blocks: the 2^14 merge-level tile where it
+// adds no multi-way pass, from 2^25 up; the 2^15 network tile otherwise.  One
+// box, 2 x 10 sorts each (profiles/r04/sortmerge): 2^30 (16 levels after the
+// 2^14 tile, 15 after 2^15: four passes either way) SORT pass 4.97 -> 3.61 ms,
+// 73.0 -> 76.8 Gkeys/s; 2^28 +4 %; 2^24 (4,3,3 vs 3,3,3 levels) -2 %; 2^27
+// would take a fifth pass.
+inline int sort_tile_u32(int k) {
+    const int knob = plan_knobs().sort_tile_u32;
+    if (knob == SORT_LT_MERGE || knob == SORT_LT_U32) return knob;
+    if (k < 25) return SORT_LT_U32;
+    return plan_uncached(k, 4, SORT_LT_MERGE).size() <= plan_uncached(k, 4, SORT_LT_U32).size() ? SORT_LT_MERGE
+                                                                                              : SORT_LT_U32;
+}
+
 // Cached per (key type, ceil_log2(n)): the knobs are read once per process.
 template <typename K>
 const std::vector<Pass>& plan_for(int64_t n) {
@@ -737,29 +842,33 @@ const std::vector<Pass>& plan_for(int64_t n) {
     static std::vector<Pass> cache[64];
     const int k = ceil_log2(n);
     std::lock_guard<std::mutex> g(mu);
-    if (cache[k].empty()) cache[k] = plan_uncached(k, (int)sizeof(K), KT<K>::LT);
+    if (cache[k].empty()) cache[k] = plan_uncached(k, (int)sizeof(K), sizeof(K) == 4 ? sort_tile_u32(k) : KT<K>::LT);
     return cache[k];
 }
 
+// lt: the u32 tile (a plan's SORT record: hi + 1); u64 has one tile.
 template <typename K>
-void launch_sort(const K* src, K* dst, int64_t n, bool ord_in, hipStream_t s, void* fence = nullptr, int flk = 0,
-                 hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
+void launch_sort(const K* src, K* dst, int64_t n, bool ord_in, hipStream_t s, int lt, void* fence = nullptr,
+                 int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     constexpr int LT = KT<K>::LT;
     if constexpr (sizeof(K) == 8) {
+        (void)lt;
         if (ord_in) launch_sort_tile<K, LT, true>(src, dst, n, s, fence, flk, ea, eb);
         else launch_sort_tile<K, LT, false>(src, dst, n, s, fence, flk, ea, eb);
+    } else if (lt == SORT_LT_MERGE) {
+        launch_sort_u32<SORT_LT_MERGE>(src, dst, n, s, (uint64_t*)fence, flk, ea, eb);
     } else {
-        launch_sort_u32(src, dst, n, s, (uint64_t*)fence, flk, ea, eb);
+        launch_sort_u32<SORT_LT_U32>(src, dst, n, s, (uint64_t*)fence, flk, ea, eb);
     }
 }
 
 template <typename K>
 hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
                            LaunchHook* hook, const StageIO* io) {
-    constexpr int LT = KT<K>::LT;
     // merge passes ping-pong between out and scratch
     if (scratch == nullptr || scratch == out || scratch == in) return hipErrorInvalidValue;
     const std::vector<Pass>& ps = plan_for<K>(n);
+    const int LT = ps[0].hi + 1;  // this plan's SORT tile
     const int np = (int)ps.size();
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
@@ -803,7 +912,7 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
                     // a merge level reads across chunks: whole input, output range [k0, k1)
                     if (merge_level<K>(src, dst, n, p.hi, s, k0, k1) != hipSuccess) return hipErrorInvalidValue;
                 } else {
-                    launch_sort<K>(src + k0, dst + k0, k1 - k0, ord_in, s);
+                    launch_sort<K>(src + k0, dst + k0, k1 - k0, ord_in, s, LT);
                 }
                 if (cout && io->after_last(k0, k1, s)) return hipErrorUnknown;
             }
@@ -818,7 +927,7 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
                 f = mergek_fence_buffer(n, (int)sizeof(K), 0, s);
                 if (!f) return hipErrorOutOfMemory;
             }
-            launch_sort<K>(src, dst, n, ord_in, s, f, f ? ps[1].R : 0, ea, eb);
+            launch_sort<K>(src, dst, n, ord_in, s, LT, f, f ? ps[1].R : 0, ea, eb);
         }
         src = dst;
     }
@@ -837,7 +946,7 @@ hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, h
 }
 
 // One pass of a plan's shape (probes and tests): the SORT tile pass over n keys
-// (kind KIND_TILE_SORT), one merge level of runs of 2^hi (KIND_RUNS), or R
+// (kind KIND_TILE_SORT; u32: hi = 13 the 2^14 tile, else 2^15), one merge level of runs of 2^hi (KIND_RUNS), or R
 // multi-way levels from runs of 2^hi (KIND_RUNSK, R = 1..4; 0: 2).
 template <typename K>
 hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int flip, hipStream_t s) {
@@ -846,7 +955,7 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
     if (kind == KIND_RUNS) return merge_level<K>(in, out, n, hi, s);
     if (kind == KIND_RUNSK) return merge_levelk(in, out, n, hi, R > 0 ? R : 2, s, 0, true, 0);
     if (kind != KIND_TILE_SORT) return hipErrorInvalidValue;
-    launch_sort<K>(in, out, n, false, s);
+    launch_sort<K>(in, out, n, false, s, hi + 1 == SORT_LT_MERGE ? SORT_LT_MERGE : KT<K>::LT);
     return hipGetLastError();
 }
 

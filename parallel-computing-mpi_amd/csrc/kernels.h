@@ -116,7 +116,7 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
 // per-stream fence buffers holds this pass's fences; gather = build them from
 // src first (the pass after a non-multi-way pass); lk_next > 0 = write the
 // fences of the next multi-way pass (runs of 2^(lw+lk), groups of 2^lk_next)
-// into the other buffer.  15 <= lw, lw + lk <= 30; src != dst; buffers 16-byte
+// into the other buffer.  SORT_LT_MERGE <= lw, lw + lk <= 30; src != dst; buffers 16-byte
 // aligned.
 hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next, LaunchHook* hook = nullptr);
@@ -130,6 +130,12 @@ int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
 #define MISORT_MK_FG_LOG2 7
 #endif
 constexpr int MERGEK_FENCE_LOG2 = MISORT_MK_FG_LOG2;
+// log2 keys of the u32 SORT tiles (bitonic.h).  15: 1024 lanes, one
+// workgroup per CU, all 15 levels as the bitonic network.  14: 512 lanes, two
+// workgroups per CU, levels 12..14 as in-LDS merge levels (MISORT_SORT_MERGE).
+// The plan picks per size (sort_tile_u32); u32 multi-way passes take runs of
+// 2^14 and up.
+constexpr int SORT_LT_U32 = 15, SORT_LT_MERGE = 14;
 // The per-stream fence buffer `phase` of a multi-way pass over n keys (the
 // one merge_levelk reads with that phase), for a SORT pass that writes the
 // first pass's fences itself; null on allocation failure.

@@ -17,6 +17,7 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_GRID_MULT", grid_mult);
     env("MISORT_MULTIWAY", multiway);
     env("MISORT_MULTIWAY_U64", multiway_u64);
+    env("MISORT_SORT_TILE_U32", sort_tile_u32);
     if (grid_mult < 1) grid_mult = 1;
 }
 
@@ -25,7 +26,7 @@ const PlanKnobs& plan_knobs() {
     return k;
 }
 
-// SORT tile per key type (log2 keys).
+// The largest SORT tile per key type (log2 keys): every plan's tiles divide it.
 int tile_log2(int key_bytes) { return key_bytes == 4 ? KT<uint32_t>::LT : KT<uint64_t>::LT; }
 
 int plan_passes(int64_t n, int key_bytes, int* out, int max) {

@@ -1,0 +1,365 @@
+// lds_merge.h -- the in-LDS merge machinery shared by the multi-way merge
+// passes (runsk.hip, k_mergek) and the u32 SORT tile's merge levels
+// (bitonic.h): merge-path co-rank searches, the per-lane merge chains, and the
+// level loop that merges K sorted sequences already in LDS pairwise in LK
+// levels.  Every sequence is followed by G words of MAX (sentinels), so the
+// chains need no end checks.
+#pragma once
+#include "kernels.h"
+
+namespace misort {
+namespace {
+
+template <typename KEY>
+constexpr KEY KMAX = (KEY)~(KEY)0;
+
+template <typename KEY>
+using kvec = KEY __attribute__((ext_vector_type(16 / sizeof(KEY))));  // 16 bytes of keys
+template <typename KEY>
+using kvec2 = KEY __attribute__((ext_vector_type(2)));
+
+template <typename KEY>
+using lds_t = __attribute__((address_space(3))) KEY;
+
+template <typename KEY>
+__device__ __forceinline__ uint32_t lds_addr(const KEY* p) {
+    return (uint32_t)(uintptr_t)(const lds_t<KEY>*)p;
+}
+template <typename KEY>
+__device__ __forceinline__ KEY lds_ld(uint32_t a) {
+    return *(const lds_t<KEY>*)(uintptr_t)a;
+}
+
+// Merge-path co-rank: a valid split of the first d outputs of merge(A, B)
+// (every A key before it <= every B key after it and vice versa; any such
+// split gives the same output values -- the keys carry no payload).  The
+// largest base in [lo, hi] with A[i - 1] <= B[d - i] for every i <= base, by
+// power-of-two steps with clamped probes, no data-dependent branches: the
+// steps 2^j <= maxr + PH, a uniform bound on hi - lo (<= min(LA, LB)) plus the
+// phase, sum to >= hi - lo + PH.  Probe addresses stay inside [A0 - 1, A0 + LA)
+// and [B0, B0 + LB].
+//
+// Phase (MISORT_MK_PHASE): lane l of each 32-lane LDS group starts its search
+// at lo - (l % 32) (positions <= lo count as true: the answer is >= lo).  With
+// a common start, lanes whose bases differ at a coarse step differ by a
+// multiple of 2 * step, so their A probes land in ONE bank (step >= 16): the
+// searches were k_mergek's largest LDS cost (SQ probe modes,
+// profiles/r04/sq_attr: 5 conflict cycles per probe instruction, more wave
+// cycles than the merge chains).  The phases put those probes on distinct
+// banks, and the B probes at (IT + 1) * l on distinct banks too.  Measured
+// on one box (profiles/r04/phase): u32 k_mergek 2524 -> 2435 us per 2^30
+// pass, 571 -> 545 at 2^28 (SQ: 3.1 -> 1.6 conflict cycles per search probe);
+// u64 (two-bank keys, 4 waves per SIMD) 2667 -> 2739 us, so u64 keeps a
+// common start.
+#ifndef MISORT_MK_PHASE
+#define MISORT_MK_PHASE 1
+#endif
+// 2: clamped probes, one compare per step (co_rank); 1: the range checks as
+// exec-mask branches (round 3)
+#ifndef MISORT_MK_COR
+#define MISORT_MK_COR 2
+#endif
+template <typename KEY, int MAXR>
+__device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
+    // first co-rank step: the largest power of two <= MAXR + PH (MAXR: a
+    // compile-time bound on hi - lo, the steps must be powers of two for the
+    // lifting search); steps above maxr + PH (uniform) are skipped
+    constexpr int PH = MISORT_MK_PHASE && sizeof(KEY) == 4 ? 31 : 0;
+    constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(MAXR + PH)));
+    static_assert(MAXR + PH <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
+    const int lo = d - LB > 0 ? d - LB : 0;
+    const int hi = d < LA ? d : LA;
+    const KEY* a = s + A0 - 1;
+    const KEY* b = s + B0 + d;
+    int base = lo - (PH ? (int)(__lane_id() & 31) : 0);
+    if constexpr (MISORT_MK_COR == 2) {
+        // every probe clamped into [lo, hi], both loads unconditional: a
+        // probe at hi that holds makes hi the answer (later probes repeat
+        // it); a step that ends below lo tests lo, which holds by definition
+        // (the answer is >= lo) and moves base up to lo, within the steps
+        // left.  No exec-mask branches; with a common start (PH = 0) no step
+        // ends below lo.
+#pragma unroll
+        for (int step = CO_STEP0; step >= 1; step >>= 1) {
+            if (step > maxr + PH) continue;  // uniform
+            const int t = base + step;
+            int i;  // clamp(t, lo, hi) (the compiler emits min + cmp + cndmask)
+            asm("v_med3_i32 %0, %1, %2, %3" : "=v"(i) : "v"(t), "v"(lo), "v"(hi));
+            const bool ok = (PH != 0 && i == lo) | (a[i] <= b[-i]);
+            base = ok ? i : base;
+        }
+        return base > lo ? base : lo;
+    }
+#pragma unroll
+    for (int step = CO_STEP0; step >= 1; step >>= 1) {
+        if (step > maxr + PH) continue;  // uniform
+        const int i = base + step;
+        if constexpr (PH) {
+            const int ic = i < lo ? lo : (i < hi ? i : hi);  // v_med3_i32
+            const bool ok = i <= lo || (i <= hi && a[ic] <= b[-ic]);
+            base = ok ? i : base;
+        } else {
+            const int ic = i < hi ? i : hi;
+            const bool ok = i <= hi && a[ic] <= b[-ic];
+            base = ok ? i : base;
+        }
+    }
+    return base;
+}
+
+// IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
+// both followed by sentinels.  A chain holds h, the head of the side it took
+// last, and g, the other side's head: each step outputs min(h, g), keeps
+// max(h, g) as the other head and reads the next key of the side it took
+// (swapping the two read pointers when that side changes) -- six VALU ops and
+// one LDS read per output (u32).  Ties may go either way: equal keys are
+// identical.  Past the end of both sequences a chain outputs MAX (their
+// sentinels).
+template <typename KEY, int IT, int MAXR>
+__device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                            KEY (&r)[IT]) {
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
+    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
+    // byte addresses of the two heads (LDS pointers are 32-bit)
+    uint32_t px = lds_addr<KEY>(s + A0 + ia), py = lds_addr<KEY>(s + B0 + dc - ia);
+    KEY h = lds_ld<KEY>(px), g = lds_ld<KEY>(py);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const bool keep = h <= g;
+        KEY o;
+        if constexpr (sizeof(KEY) == 4) {
+            r[k] = min(h, g);
+            o = max(h, g);
+        } else {  // no 64-bit min/max: selects on the compare (the compiler
+                  // emits umin + umax, two v_cmp_u64; hiding the compared values
+                  // from it, as cx<u64> does, measured 5 % slower here:
+                  // 2.52 -> 2.64 ms per 16-way pass at 2^29, profiles/r03/ab2)
+            r[k] = keep ? h : g;
+            o = keep ? g : h;
+        }
+        const uint32_t nx = keep ? px : py;
+        py = keep ? py : px;
+        px = nx + (uint32_t)sizeof(KEY);
+        h = lds_ld<KEY>(px);
+        g = o;
+    }
+}
+
+// Two consecutive keys at LDS byte address a.  MISORT_MK_CHAIN 2: one
+// ds_read_b64 (u32) / ds_read_b128 (u64) at the key's own alignment -- the
+// type claims the vector's alignment so the compiler selects the single wide
+// read, which the unaligned LDS mode of the HSA queues serves; 1: the
+// compiler's choice for a key-aligned pair (ds_read2_b32 / ds_read2_b64, two
+// LDS accesses).
+template <typename KEY, bool WIDE>
+__device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
+    if constexpr (WIDE) {
+        return *(const __attribute__((address_space(3))) kvec2<KEY>*)(uintptr_t)a;
+    } else {
+        typedef KEY v2 __attribute__((ext_vector_type(2), aligned(sizeof(KEY))));
+        const v2 v = *(const __attribute__((address_space(3))) v2*)(uintptr_t)a;
+        return kvec2<KEY>{v.x, v.y};
+    }
+}
+
+// The four keys of two ascending pairs (v0 <= v1, n0 <= n1) in order:
+// s0 = min(v0, n0), s3 = max(v1, n1), and with a = max(v0, n0) <= max(v1, n1)
+// the middle two are min(a, min(v1, n1)) and max(a, min(v1, n1)) -- for u32
+// a v_min_u32, v_max_u32, v_min3_u32, v_med3_u32 and v_max_u32; for u64 three
+// compares, each selecting both of its outputs.
+[[maybe_unused]] __device__ __forceinline__ void merge4(uint32_t v0, uint32_t v1, uint32_t n0, uint32_t n1, uint32_t& s0, uint32_t& s1,
+                                       uint32_t& s2, uint32_t& s3) {
+    s0 = min(v0, n0);
+    const uint32_t a = max(v0, n0);
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(s1) : "v"(a), "v"(v1), "v"(n1));  // (not formed from min(min()))
+    s2 = max(min(a, v1), min(max(a, v1), n1));  // v_med3_u32
+    s3 = max(v1, n1);
+}
+[[maybe_unused]] __device__ __forceinline__ void merge4(uint64_t v0, uint64_t v1, uint64_t n0, uint64_t n1, uint64_t& s0, uint64_t& s1,
+                                       uint64_t& s2, uint64_t& s3) {
+    const bool c0 = v0 < n0, c1 = v1 < n1;
+    s0 = c0 ? v0 : n0;
+    const uint64_t a = c0 ? n0 : v0, m = c1 ? v1 : n1;
+    s3 = c1 ? n1 : v1;
+    const bool c2 = a < m;
+    s1 = c2 ? a : m;
+    s2 = c2 ? m : a;
+}
+
+// The same IT outputs as merge_chain, two per step from blocks of two keys
+// (a vector merge, as in Inoue et al.'s AA-sort).  The lane holds v0 <= v1,
+// the two largest keys it has read and not yet output; v1, the largest key
+// read, is the last key read from one side (L), so every unread key of L is
+// >= v1, and the next two outputs are the lowest two of v and the next two
+// keys of the other side (S).  A step reads those two keys (one LDS read),
+// outputs the lowest two of the four and keeps the upper two; when the block's
+// second key exceeds v1 the sides swap roles (the block's side now holds the
+// largest key read).  Five VALU ops of merging and four of pointers per two
+// outputs (u32) -- the one-key chain spends six VALU and an LDS read per
+// output.  A side gives at most IT keys, so the G >= IT sentinels after each
+// sequence cover every read.
+template <typename KEY, int IT, bool WIDE, int MAXR>
+__device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                                KEY (&r)[IT]) {
+    static_assert(IT % 2 == 0, "two outputs per step");
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;
+    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
+    constexpr uint32_t B2 = 2 * sizeof(KEY);
+    const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
+    const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
+    // S: the side whose last read key is the smaller (ties: either)
+    const bool as = a.y <= b.y;
+    uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
+    KEY v0, v1;
+    merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
+#pragma unroll
+    for (int k = 1; k < IT / 2; ++k) {
+        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(ps);
+        ps += B2;
+        const bool sw = n.y > v1;
+        merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
+        const uint32_t t = sw ? pl : ps;
+        pl = sw ? ps : pl;
+        ps = t;
+    }
+}
+
+// merge_chain_blk with ALIGNED two-key reads (chain 3: one ds_read_b64 for u32,
+// ds_read_b128 for u64, at the pair's own alignment -- the unaligned forms
+// measured 2.2x slower).  Every sequence starts at an even LDS slot, and the
+// lane starts each side at the aligned pair holding its first key: when that
+// key is the pair's second, the pair's first key is an earlier output -- <=
+// every key this lane outputs (A[ia-1] <= B[ib] by the co-rank, B[ib-1] <
+// A[ia] by its maximality) -- so it leaves the merge first.  The lane merges
+// RN >= IT + 2 keys (even); its outputs are r[ex, ex + IT), ex = the early
+// keys (0..2).  A side gives at most RN keys from its pair, so G >= RN
+// sentinels.  IT may be odd (the lanes' diagonals then fall on distinct banks).
+template <typename KEY, int IT, int RN, int MAXR>
+__device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
+                                              KEY (&r)[RN]) {
+    static_assert(RN % 2 == 0 && RN >= IT + 2, "two outputs per step, two early keys");
+    const int tot = LA + LB;
+    const int dc = d < tot ? d : tot;
+    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
+    const int ib = dc - ia;
+    constexpr uint32_t B2 = 2 * sizeof(KEY);
+    const uint32_t pa = lds_addr<KEY>(s + A0 + (ia & ~1)), pb = lds_addr<KEY>(s + B0 + (ib & ~1));
+    const kvec2<KEY> a = lds_ld2<KEY, true>(pa), b = lds_ld2<KEY, true>(pb);
+    const bool as = a.y <= b.y;
+    uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
+    KEY v0, v1;
+    merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
+#pragma unroll
+    for (int k = 1; k < RN / 2; ++k) {
+        const kvec2<KEY> n = lds_ld2<KEY, true>(ps);
+        ps += B2;
+        const bool sw = n.y > v1;
+        merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
+        const uint32_t t = sw ? pl : ps;
+        pl = sw ? ps : pl;
+        ps = t;
+    }
+    return (ia & 1) + (ib & 1);
+}
+
+// The in-LDS levels: K sequences at st[q] (length ln[q], each followed by G
+// sentinels) merged pairwise in LK levels by NT lanes of IT outputs each.
+// Level lv writes pair p's output at qp[p] (a multiple of QA past the
+// previous pair's sentinels) with G sentinels after it; the last level's
+// outputs stay in registers: lane tid holds outputs [tid * IT, tid * IT + IT)
+// of the merged sequence as r[ex, ex + IT).  S (a shape): K, LKS, NT, IT, G,
+// QA, RN (registers per lane: IT, or more for chains that merge extra keys),
+// CH (chain: 0 one key per read, 1/2 two, 3 aligned pairs), MAXR (bound on a
+// pair's shorter sequence).  MODE (probes): 1 = no merging, 2 = first level
+// only, 3 = co-rank searches without chains.  Ends with a barrier after the
+// last level's reads (the caller may then overwrite the LDS).
+template <typename KEY, typename S, int MODE>
+__device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&ln)[S::K], KEY (&r)[S::RN], int& ex,
+                                                 int tid, int LAST) {
+    constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, RN = S::RN, CH = S::CH;
+    constexpr KEY MAXK = KMAX<KEY>;
+    ex = 0;
+    const int pos = tid * IT;
+    const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
+#pragma unroll
+    for (int lv = 1; lv <= LK; ++lv) {
+        const int P = K >> lv;  // pairs merged at this level
+        // pair p's output: [qp[p], qp[p] + lp[p]), then G sentinels; the next
+        // pair starts at the first lane boundary past them
+        int qp[K / 2], lp[K / 2];
+        int qa = 0, maxr = 0;  // maxr: the longest co-rank range of the level's pairs (uniform)
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const int mr = ln[2 * p] < ln[2 * p + 1] ? ln[2 * p] : ln[2 * p + 1];
+            maxr = mr > maxr ? mr : maxr;
+            lp[p] = ln[2 * p] + ln[2 * p + 1];
+            qp[p] = qa;
+            qa = (qa + lp[p] + G + S::QA - 1) / S::QA * S::QA;
+        }
+        // the lane's pair: the last one starting at or before pos
+        int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
+#pragma unroll
+        for (int p = 1; p < P; ++p) {
+            const bool in = pos >= qp[p];
+            A0 = in ? st[2 * p] : A0;
+            LA = in ? ln[2 * p] : LA;
+            B0 = in ? st[2 * p + 1] : B0;
+            LB = in ? ln[2 * p + 1] : LB;
+            Q = in ? qp[p] : Q;
+            LP = in ? lp[p] : LP;
+        }
+        const int end = qp[P - 1] + lp[P - 1];
+        if (MODE == 1 || (MODE == 2 && lv > 1) || MODE == 3) {
+            ex = 0;
+#pragma unroll
+            for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
+            if (MODE == 3 && wpos < end) {  // the search alone, its result kept alive
+                const int dc = pos - Q < LA + LB ? pos - Q : LA + LB;
+                r[0] ^= (KEY)(co_rank<KEY, S::MAXR>(s, A0, LA, B0, LB, dc, maxr) & 1);
+            }
+        } else if (wpos < end) {
+            if constexpr (CH == 0)
+                merge_chain<KEY, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            else if constexpr (CH == 3)
+                ex = merge_chain_al<KEY, IT, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+            else
+                merge_chain_blk<KEY, RN, CH == 2, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+        }
+        __syncthreads();
+        if (lv < LK) {
+            // a lane's outputs past its pair's end are MAX (the chain ran into
+            // the sentinels), the value the sentinel stores write there too
+            if (pos < Q + LP) {
+                if constexpr (CH == 3 || IT % 2) {
+                    // output j is r[ex + j]: one store per key from base pos - ex
+                    KEY* q = s + pos - ex;
+#pragma unroll
+                    for (int k = 0; k < RN; ++k)
+                        if (k >= ex && k < ex + IT) q[k] = r[k];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < IT; j += 2)
+                        *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
+                }
+            }
+            for (int x = tid; x < P * G; x += NT) {
+                const int p = x / G;
+                int e = 0;
+#pragma unroll
+                for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
+                s[e + (x - p * G)] = MAXK;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                st[p] = qp[p];
+                ln[p] = lp[p];
+            }
+        }
+    }
+}
+
+}  // namespace
+}  // namespace misort

@@ -97,8 +97,8 @@ def test_merge_level_duplicates_and_single_run(ctx, dt):
 
 
 @pytest.mark.parametrize("lk", [1, 2, 3, 4])
-@pytest.mark.parametrize("dt,hi", [(np.uint32, 15), (np.uint32, 16), (np.uint32, 17), (np.uint64, 13),
-                                   (np.uint64, 14), (np.uint64, 16)])
+@pytest.mark.parametrize("dt,hi", [(np.uint32, 14), (np.uint32, 15), (np.uint32, 16), (np.uint32, 17),
+                                   (np.uint64, 13), (np.uint64, 14), (np.uint64, 16)])
 @pytest.mark.parametrize("n", [(1 << 20) + 3, (1 << 19), (1 << 19) - 4097, 3 * (1 << 17) + 5, 5000, 12345, 2049])
 def test_mergek_level_matches_numpy(ctx, lk, dt, hi, n):
     """One 2^lk-way pass (runsk.hip): groups of 2^lk runs merged, ragged last
@@ -109,7 +109,7 @@ def test_mergek_level_matches_numpy(ctx, lk, dt, hi, n):
 
 
 @pytest.mark.parametrize("lk", [1, 2, 3, 4])
-@pytest.mark.parametrize("dt,hi", [(np.uint32, 15), (np.uint32, 16), (np.uint32, 21), (np.uint64, 13),
+@pytest.mark.parametrize("dt,hi", [(np.uint32, 14), (np.uint32, 16), (np.uint32, 21), (np.uint64, 13),
                                    (np.uint64, 16), (np.uint64, 19)])
 def test_mergek_level_ties_and_edges(ctx, lk, dt, hi):
     """Duplicate-heavy, all-equal (every fence the same key: chunks cut by
@@ -145,7 +145,7 @@ def test_merge_level_rejects_bad_shapes(ctx):
     for hi in (5, 11):  # runs shorter than the merge tile
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi)
-    for hi, lk in ((11, 2), (14, 2), (15, 5)):  # multi-way: runs shorter than a SORT tile; lk > 4
+    for hi, lk in ((11, 2), (13, 2), (15, 5)):  # multi-way: runs shorter than the 2^14 SORT tile; lk > 4
         with pytest.raises(misort.MisortError):
             run_level(ctx, x, hi, "run_mergek", lk)
     x64 = np.arange(1 << 16, dtype=np.uint64)
@@ -181,7 +181,7 @@ a = out.view(iv).cpu().numpy().view(dt)
 b = d.view(iv).cpu().numpy().view(dt)
 ref = np.sort(keys)
 ok = np.array_equal(a, ref) and np.array_equal(b, ref)
-print("RUNS", sum(1 for p in plan if p[0] == "run_merge") + sum(p[2] for p in plan if p[0] == "run_mergek"),
+print("TILE", plan[0][1] + 1, "RUNS", sum(1 for p in plan if p[0] == "run_merge") + sum(p[2] for p in plan if p[0] == "run_mergek"),
       "RUNSK", sum(1 for p in plan if p[0] == "run_mergek"), "OK" if ok else "MISMATCH")
 ctx.close()
 """
@@ -196,9 +196,14 @@ ctx.close()
     (4, {"MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),
     (4, {"MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
     (4, {"MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
-    (4, {}, (1 << 27) + 777),  # the default: three 16-way passes
-    (4, {}, (1 << 25) + 3),  # 3 + 3 + 2 + 2 levels
-    (4, {"MISORT_MULTIWAY": "4"}, (1 << 25) + 3),  # 4 + 3 + 3 levels (16-way)
+    (4, {}, (1 << 27) + 777),  # the default: 2^14 tiles, four 16-way passes
+    (4, {}, (1 << 26) + 777),  # 2^15 tiles (2^14 ones would add a pass): three 16-way passes
+    (4, {}, (1 << 25) + 3),  # 2^14 merge-level tiles, 4 + 4 + 4 levels
+    (4, {"MISORT_SORT_TILE_U32": "15"}, (1 << 25) + 3),  # 2^15 tiles, 4 + 4 + 3 levels
+    (4, {"MISORT_SORT_TILE_U32": "14"}, (1 << 22) + 4099),  # 2^14 tiles at a size that defaults to 2^15
+    (4, {"MISORT_SORT_TILE_U32": "14"}, (1 << 14) + 1),  # one level past the 2^14 tile: a 2-way pass
+    (4, {"MISORT_SORT_TILE_U32": "14"}, 3 * (1 << 14) - 5),  # a full tile + a partial one
+    (4, {"MISORT_SORT_TILE_U32": "14", "MISORT_MULTIWAY": "3"}, (1 << 24) + 12345),
     (4, {}, 3 * (1 << 23) + 5),
     (4, {}, (1 << 17) + 1),  # one level past the tile: a 2-way pass
     (4, {}, (1 << 16) + 3),
@@ -222,12 +227,13 @@ ctx.close()
 def test_full_sort_merge_passes(kb, env, n):
     """The whole local sort (SORT tile, then merge passes) under the planner
     knobs, against np.sort; the plan has the fewest multi-way passes for the
-    levels past the tile (u32: 2^15 keys, u64: 2^13)."""
+    levels past the tile (u32: 2^14 keys from 2^25 where that adds no pass,
+    else 2^15; u64: 2^13)."""
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
                         str(kb)], env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    line = [x for x in r.stdout.splitlines() if x.startswith("RUNS")][-1]
-    _, count, _, countk, verdict = line.split()
+    line = [x for x in r.stdout.splitlines() if x.startswith("TILE")][-1]
+    _, tile, _, count, _, countk, verdict = line.split()
     assert verdict == "OK", line
     if kb == 4:  # default: the fewest passes of up to 16-way
         cap = int(env["MISORT_MULTIWAY"]) if "MISORT_MULTIWAY" in env else 4
@@ -237,4 +243,12 @@ def test_full_sort_merge_passes(kb, env, n):
         assert int(countk) == -(-int(count) // cap)  # the fewest multi-way passes
     else:
         assert int(countk) == 0
-    assert int(count) == max(0, (n - 1).bit_length() - (15 if kb == 4 else 13))
+    if kb == 8:
+        assert int(tile) == 13
+    elif "MISORT_SORT_TILE_U32" in env:
+        assert int(tile) == int(env["MISORT_SORT_TILE_U32"])
+    elif not env:
+        assert int(tile) == misort.plan(n, 4)[0][1] + 1  # this process has the default knobs
+    else:
+        assert int(tile) in (14, 15)
+    assert int(count) == max(0, (n - 1).bit_length() - int(tile))

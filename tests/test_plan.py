@@ -1,7 +1,8 @@
 """The local-sort plan (bitonic.h plan_uncached) on the CPU.
 
 A local sort (the reference's std::sort, psort.cc:175) is one SORT pass of
-2^LT-key bitonic tiles (u32: 2^15, u64: 2^13) followed by merge passes:
+2^LT-key tiles (u32: 2^14 or 2^15 by size, u64: 2^13; the plan's SORT record
+carries it as hi = LT - 1) followed by merge passes:
 2^lk-way passes of lk levels each (runsk.hip) and 2-way passes of one level
 (runs.hip).  A plan is right when
   * it starts with the SORT pass and its merge passes finish exactly the levels
@@ -34,9 +35,10 @@ def merge_levels(plan):
     return out
 
 
-def replay(keys, plan, lt):
+def replay(keys, plan):
     """The plan on a numpy model: the SORT pass sorts every 2^lt tile, each
     merge pass sorts neighbouring groups of runs (all-ones padding to 2^k)."""
+    lt = plan[0][1] + 1
     n = keys.size
     k = max(ceil_log2(n), lt)
     x = np.full(1 << k, np.iinfo(keys.dtype).max, dtype=keys.dtype)
@@ -54,11 +56,14 @@ SIZES = [1, 2, 31, 1000, (1 << 13) + 1, (1 << 15) - 3, 1 << 15, (1 << 15) + 1, 1
 @pytest.mark.parametrize("key_bytes", [4, 8])
 @pytest.mark.parametrize("n", SIZES)
 def test_plan_covers_the_levels(n, key_bytes):
-    lt = misort.tile_log2(key_bytes)
-    assert lt == (15 if key_bytes == 4 else 13)
+    assert misort.tile_log2(key_bytes) == (15 if key_bytes == 4 else 13)  # the largest tile
     p = misort.plan(n, key_bytes)
     assert p[0][0] == KIND_SORT
+    lt = p[0][1] + 1
     k = ceil_log2(n)
+    assert lt in ((14, 15) if key_bytes == 4 else (13,))
+    if key_bytes == 4 and lt == 14:  # only from 2^25, and only where it adds no merge pass
+        assert k >= 25 and k != 27
     assert merge_levels(p) == list(range(lt, k))
     lwk_max = 30 if key_bytes == 4 else 29  # 32-bit row offsets of a multi-way group
     for kind, hi, r, _ in p[1:]:
@@ -67,18 +72,22 @@ def test_plan_covers_the_levels(n, key_bytes):
 
 
 def test_plan_pass_counts():
-    # 2^30 u32: 1 SORT + four multi-way passes (levels 16..30: three 16-way
-    # and one 8-way; one 2-way merge pass per level would be 1 + 15)
+    # 2^30 u32: 2^14-key SORT tiles + four 16-way passes (levels 15..30; one
+    # 2-way merge pass per level would be 1 + 16)
     p30 = misort.plan(1 << 30, 4)
-    assert p30[0][0] == KIND_SORT
-    assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 15, 4), (KIND_RUNSK, 19, 4), (KIND_RUNSK, 23, 4),
-                                                (KIND_RUNSK, 27, 3)]
+    assert tuple(p30[0][:2]) == (KIND_SORT, 13)
+    assert [tuple(q[:3]) for q in p30[1:]] == [(KIND_RUNSK, 14, 4), (KIND_RUNSK, 18, 4), (KIND_RUNSK, 22, 4),
+                                                (KIND_RUNSK, 26, 4)]
     # the fewest passes of at most four levels (16-way) at every size
-    # (profiles/r04/mw: faster than 8-way passes from 2^26 to 2^31)
-    assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [4, 3, 3, 3]
-    assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [4, 4, 3, 3]
+    # (profiles/r04/mw: faster than 8-way passes from 2^26 to 2^31); the
+    # 2^14 tile from 2^25 where it adds no pass (profiles/r04/sortmerge)
+    assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [4, 4, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [4, 4, 4, 3]
+    assert [q[1] for q in misort.plan(1 << 27, 4)] == [14, 15, 19, 23]  # 2^15 tiles: 2^14 ones would add a pass
     assert [q[2] for q in misort.plan(1 << 27, 4)[1:]] == [4, 4, 4]
-    assert [q[2] for q in misort.plan(1 << 25, 4)[1:]] == [4, 3, 3]
+    assert [q[2] for q in misort.plan(1 << 25, 4)[1:]] == [4, 4, 3]
+    assert [q[2] for q in misort.plan(1 << 26, 4)[1:]] == [4, 4, 4]
+    assert misort.plan(1 << 24, 4)[0][1] == 14  # below 2^25: 2^15 tiles
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 4 + [KIND_RUNS]
     # small u32 sorts take the merge passes too (round 3: they beat the bitonic
@@ -101,12 +110,11 @@ def test_plan_pass_counts():
 @pytest.mark.parametrize("key_bytes", [4, 8])
 @pytest.mark.parametrize("n", [1000, (1 << 15) + 1, 1 << 16, 100003, (1 << 18) - 5, 1 << 19, (1 << 21) + 3])
 def test_plan_replay_sorts(n, key_bytes):
-    lt = misort.tile_log2(key_bytes)
     dt = np.uint32 if key_bytes == 4 else np.uint64
     rng = np.random.default_rng(n)
     keys = rng.integers(0, np.iinfo(dt).max, size=n, dtype=dt, endpoint=True)
     keys[::7] = keys[3]  # duplicates
-    got = replay(keys, misort.plan(n, key_bytes), lt)
+    got = replay(keys, misort.plan(n, key_bytes))
     np.testing.assert_array_equal(got, np.sort(keys))
 
 
@@ -137,9 +145,30 @@ def test_pass_width_knobs(mw):
         for kb in (4, 8):
             p = plans[f"{n}_{kb}"]
             assert p[0][0] == KIND_SORT
-            assert merge_levels(p) == list(range(15 if kb == 4 else 13, ceil_log2(n)))
+            assert merge_levels(p) == list(range(p[0][1] + 1, ceil_log2(n)))
             widths = [q[2] for q in p[1:] if q[0] == KIND_RUNSK]
             if int(mw) < 2:
                 assert not widths
             else:
                 assert widths and max(widths) <= int(mw)
+
+
+@pytest.mark.parametrize("tile", ["14", "15"])
+def test_sort_tile_knob(tile):
+    """MISORT_SORT_TILE_U32 pins the u32 SORT tile at every size."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sizes = [(1 << 14) + 1, (1 << 20) + 3, 1 << 27, 1 << 30]
+    r = subprocess.run([sys.executable, "-c", PLAN_CHILD, os.path.join(root, "parallel-computing-mpi_amd"),
+                        ",".join(map(str, sizes))], env=dict(os.environ, MISORT_SORT_TILE_U32=tile),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plans = json.loads(r.stdout.strip().splitlines()[-1])
+    for n in sizes:
+        p = plans[f"{n}_4"]
+        assert p[0][1] + 1 == int(tile)
+        assert merge_levels(p) == list(range(int(tile), ceil_log2(n)))
+        assert plans[f"{n}_8"][0][1] == 12
