@@ -618,6 +618,12 @@ __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* i
 #ifndef MISORT_SORT_MERGE
 #define MISORT_SORT_MERGE 12
 #endif
+// Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
+// (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
+// (4) and stores what it has -- the differences price each phase.
+#ifndef MISORT_SORT_STOP
+#define MISORT_SORT_STOP 0
+#endif
 template <int LT>
 struct SortMergeShape {
     static constexpr int K = 1 << (LT - 11), LKS = LT - 11, NT = 1 << (LT - 5);  // 2^11-key runs, 32 keys per lane
@@ -688,40 +694,45 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
             for (int j = 0; j < G::V; ++j) s[pad(e + j)] = pre[k][j];
         }
         __syncthreads();
-        uint32_t x[32];
+        constexpr int STOP = MERGE ? MISORT_SORT_STOP : 0;
+        if constexpr (STOP == 0 || STOP >= 2) {
+            uint32_t x[32];
 #pragma unroll
-        for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
-        reg_stages_c<uint32_t, 0, 1, true>(x);
-        reg_stages_c<uint32_t, 1, 2, true>(x);
-        reg_stages_c<uint32_t, 2, 3, true>(x);
-        reg_stages_c<uint32_t, 3, 4, true>(x);
-        reg_stages_c<uint32_t, 4, 5, true>(x);
-        wave_levels<6, WL>(x, t & 63);
-        // each lane rewrites only the keys it read: no barrier before, and the
-        // next phase (level WL+1 <= 11) stays inside the wave
+            for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
+            reg_stages_c<uint32_t, 0, 1, true>(x);
+            reg_stages_c<uint32_t, 1, 2, true>(x);
+            reg_stages_c<uint32_t, 2, 3, true>(x);
+            reg_stages_c<uint32_t, 3, 4, true>(x);
+            reg_stages_c<uint32_t, 4, 5, true>(x);
+            wave_levels<6, WL>(x, t & 63);
+            // each lane rewrites only the keys it read: no barrier before, and the
+            // next phase (level WL+1 <= 11) stays inside the wave
 #pragma unroll
-        for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
-        if constexpr (WL + 1 <= WAVE_BITS && MISORT_SORT_WAVE_SYNC) wave_sync();
-        else __syncthreads();
+            for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
+            if constexpr (WL + 1 <= WAVE_BITS && MISORT_SORT_WAVE_SYNC) wave_sync();
+            else __syncthreads();
+        }
         // the next tile's loads fly during the LDS phases (issued here, not
         // before the wave levels, so their registers and the cross-lane
         // temporaries are never live together)
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < ntiles) sort_fetch<LT, FULL>(pre, in, nxt, n, t);
         if constexpr (MERGE) {
-            sort_levels_w<K, WL + 1, 11>(s, t);
+            if constexpr (STOP == 0 || STOP >= 3) sort_levels_w<K, WL + 1, 11>(s, t);
             // wave w's sorted run (keys w * 2^11 ...) -> plain layout at
             // w * (RUN + GS), then GS sentinels; lane l moves keys 64c + l
             // (consecutive lanes, consecutive words: no bank conflicts)
             const int w = t >> 6, l = t & 63;
-            uint32_t y[32];
+            if constexpr (STOP == 0 || STOP >= 4) {
+                uint32_t y[32];
 #pragma unroll
-            for (int c = 0; c < 32; ++c) y[c] = s[pad((w << 11) + (c << 6) + l)];
-            __syncthreads();
-            const int b0 = w * (MS::RUN + MS::GS);
+                for (int c = 0; c < 32; ++c) y[c] = s[pad((w << 11) + (c << 6) + l)];
+                __syncthreads();
+                const int b0 = w * (MS::RUN + MS::GS);
 #pragma unroll
-            for (int c = 0; c < 32; ++c) s[b0 + (c << 6) + l] = y[c];
-            if (l < MS::GS) s[b0 + MS::RUN + l] = 0xFFFFFFFFu;
+                for (int c = 0; c < 32; ++c) s[b0 + (c << 6) + l] = y[c];
+                if (l < MS::GS) s[b0 + MS::RUN + l] = 0xFFFFFFFFu;
+            }
             __syncthreads();
             int st[MS::K], ln[MS::K];
 #pragma unroll
@@ -731,10 +742,10 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
             }
             uint32_t r[MS::RN];
             int ex = 0;
-            lds_merge_levels<uint32_t, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
+            if constexpr (STOP == 0) lds_merge_levels<uint32_t, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
             // the merged tile: lane t's outputs [33 t, 33 t + 33) back to LDS
             // (the last level's reads are done), then out as 16-byte vectors
-            if (t * MS::IT < G::T) {
+            if (STOP == 0 && t * MS::IT < G::T) {
 #pragma unroll
                 for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
             }

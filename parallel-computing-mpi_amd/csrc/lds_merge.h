@@ -13,6 +13,13 @@ namespace {
 template <typename KEY>
 constexpr KEY KMAX = (KEY)~(KEY)0;
 
+// A workgroup barrier for hand-offs through LDS only: waits for this wave's
+// LDS operations, not for its global loads and stores.  __syncthreads() is a
+// workgroup fence as well, s_waitcnt vmcnt(0) before the s_barrier, which
+// would drain a prefetch of the next chunk at every merge level.  The memory
+// clobber keeps the compiler from moving memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <typename KEY>
 using kvec = KEY __attribute__((ext_vector_type(16 / sizeof(KEY))));  // 16 bytes of keys
 template <typename KEY>
@@ -327,7 +334,7 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
             else
                 merge_chain_blk<KEY, RN, CH == 2, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
-        __syncthreads();
+        lds_barrier();
         if (lv < LK) {
             // a lane's outputs past its pair's end are MAX (the chain ran into
             // the sentinels), the value the sentinel stores write there too
@@ -351,7 +358,7 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                 for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
                 s[e + (x - p * G)] = MAXK;
             }
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int p = 0; p < P; ++p) {
                 st[p] = qp[p];

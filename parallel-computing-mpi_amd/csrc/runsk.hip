@@ -883,7 +883,82 @@ __device__ __forceinline__ int row_part(int tid) {
     return __builtin_amdgcn_readfirstlane(tid) / Shape<KEY, LK>::RW;
 }
 
-// k_mergek: one workgroup per chunk.  MODE (probes only, MISORT_MK_PROBE):
+// The chunk's in-LDS work after its keys and sentinels are in LDS: the merge
+// levels, the outputs back to LDS (shifted so every 16-byte global vector is
+// one aligned LDS vector), out to HBM, and the next pass's fences.
+template <typename KEY, int LK, bool FENCES, int MODE>
+__device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY* __restrict__ dst,
+                                             typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid) {
+    typedef Shape<KEY, LK> S;
+    constexpr int K = S::K, NT = S::NT, IT = S::IT;
+    constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
+    constexpr int LAST = S::LDS_KEYS - PAD - 1;
+    const int len = d->o[K];
+    constexpr int RN = S::RN;  // chain 3: up to two leading keys not the lane's (ex)
+    KEY r[RN];
+    int ex = 0;  // the lane's outputs are r[ex, ex + IT)
+    const int pos = tid * IT;
+    // the first level's input sequences: the chunk's segments
+    int st[K], ln[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        st[q] = S::seg(d->o[q], q);
+        ln[q] = d->o[q + 1] - d->o[q];
+    }
+    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST);
+    const int64_t out0 = d->out0;
+    // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
+    // vector is one aligned LDS vector (a lane's outputs past len are MAX and
+    // land past the chunk)
+    const int sh = (int)(out0 & (VK - 1));
+    if (pos < len) {
+        KEY* q = s + sh + pos - ex;
+#pragma unroll
+        for (int k = 0; k < RN; ++k)
+            if (k >= ex && k < ex + IT) q[k] = r[k];
+    }
+    lds_barrier();
+    const int nv = (sh + len + VK - 1) / VK;
+    KEY* __restrict__ o = dst + (out0 - sh);
+    for (int v = tid; v < nv; v += NT) {
+        const int e = VK * v;
+        if (e >= sh && e + VK <= sh + len) {
+            __builtin_nontemporal_store(*reinterpret_cast<const kvec<KEY>*>(s + e), reinterpret_cast<kvec<KEY>*>(o + e));
+        } else {
+#pragma unroll
+            for (int j = 0; j < VK; ++j)
+                if (e + j >= sh && e + j < sh + len) o[e + j] = s[e + j];
+        }
+    }
+    if constexpr (FENCES) {
+        // the chunk's fences are consecutive entries of fout: one coalesced
+        // store per fence from consecutive lanes
+        const int64_t first = (out0 + FG - 1) & ~(FG - 1);
+        const int nf = first < out0 + len ? (int)((out0 + len - first + FG - 1) >> FG_LOG2) : 0;
+        if (tid < nf) {
+            const int64_t gp = first + ((int64_t)tid << FG_LOG2);
+            fout[gp >> FG_LOG2] = fpack<KEY>(s[(int)(gp - (out0 - sh))], gp, lwn, lkn);
+        }
+    }
+}
+
+// The sentinels after every segment of the chunk.
+template <typename KEY, int LK>
+__device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d, int tid) {
+    typedef Shape<KEY, LK> S;
+    // a wave per segment (uniform segment index: the descriptor's offsets come
+    // by scalar loads), G <= 64 lanes each
+    static_assert(S::G <= 64, "sentinels: one wave per segment");
+    const int lane = tid & 63;
+    for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64)
+        if (lane < S::G) s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = KMAX<KEY>;
+}
+
+// k_mergek: one workgroup per chunk.  (A persistent grid that loads the next
+// chunk into registers during the merge levels ran 2.28 -> 2.82 ms per 2^30
+// pass even with LDS-only barriers: gfx950 counts loads and stores in one
+// in-order vmcnt, so waiting for the prefetch also waits for the previous
+// chunk's stores; profiles/r04/persist.)  MODE (probes only, MISORT_MK_PROBE):
 // 0 = the pass; 1 = no merge (the access pattern's floor); 2 = level 1 only;
 // 3 = the co-rank searches of every level without the chains (for SQ
 // attribution: 3 - 1 = the searches, 0 - 3 = the chains).
@@ -894,10 +969,6 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
-    constexpr int K = S::K, NT = S::NT, IT = S::IT, G = S::G;
-    constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
-    constexpr int LAST = S::LDS_KEYS - PAD - 1;
-    constexpr KEY MAXK = KMAX<KEY>;
     __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
     KEY* s = tile + PAD;
     const int tid = threadIdx.x;
@@ -945,59 +1016,10 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
             for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         }
-        for (int e = tid; e < K * G; e += NT) {  // the sentinels after every segment
-            const int r = e / G;
-            s[S::seg(d->o[r], r) + (d->o[r + 1] - d->o[r]) + (e - r * G)] = MAXK;
-        }
+        mergek_sentinels<KEY, LK>(s, d, tid);
     }
     __syncthreads();
-    const int len = d->o[K];
-    constexpr int RN = S::RN;  // chain 3: up to two leading keys not the lane's (ex)
-    KEY r[RN];
-    int ex = 0;  // the lane's outputs are r[ex, ex + IT)
-    const int pos = tid * IT;
-    // the first level's input sequences: the chunk's segments
-    int st[K], ln[K];
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        st[q] = S::seg(d->o[q], q);
-        ln[q] = d->o[q + 1] - d->o[q];
-    }
-    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST);
-    const int64_t out0 = d->out0;
-    // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
-    // vector is one aligned LDS vector (a lane's outputs past len are MAX and
-    // land past the chunk)
-    const int sh = (int)(out0 & (VK - 1));
-    if (pos < len) {
-        KEY* q = s + sh + pos - ex;
-#pragma unroll
-        for (int k = 0; k < RN; ++k)
-            if (k >= ex && k < ex + IT) q[k] = r[k];
-    }
-    __syncthreads();
-    const int nv = (sh + len + VK - 1) / VK;
-    KEY* __restrict__ o = dst + (out0 - sh);
-    for (int v = tid; v < nv; v += NT) {
-        const int e = VK * v;
-        if (e >= sh && e + VK <= sh + len) {
-            __builtin_nontemporal_store(*reinterpret_cast<const kvec<KEY>*>(s + e), reinterpret_cast<kvec<KEY>*>(o + e));
-        } else {
-#pragma unroll
-            for (int j = 0; j < VK; ++j)
-                if (e + j >= sh && e + j < sh + len) o[e + j] = s[e + j];
-        }
-    }
-    if constexpr (FENCES) {
-        // the chunk's fences are consecutive entries of fout: one coalesced
-        // store per fence from consecutive lanes
-        const int64_t first = (out0 + FG - 1) & ~(FG - 1);
-        const int nf = first < out0 + len ? (int)((out0 + len - first + FG - 1) >> FG_LOG2) : 0;
-        if (tid < nf) {
-            const int64_t gp = first + ((int64_t)tid << FG_LOG2);
-            fout[gp >> FG_LOG2] = fpack<KEY>(s[(int)(gp - (out0 - sh))], gp, lwn, lkn);
-        }
-    }
+    mergek_chunk<KEY, LK, FENCES, MODE>(s, d, dst, fout, lwn, lkn, tid);
 }
 
 // Fence buffers, bounds and descriptors: one grow-only set per (device, stream).
@@ -1172,12 +1194,13 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const bool bound = hook && hook->binds();
     if (bound) (void)hook->bind(KIND_RUNSK_KERNEL, KIND_RUNSK, kb, &ea, &eb);
     else if (hook) hook->before(KIND_RUNSK_KERNEL, kb, s);
-    if (lk_next > 0)
+    if (lk_next > 0) {
         launch_timed(k_mergek<KEY, LK, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next);
-    else
+    } else {
         launch_timed(k_mergek<KEY, LK, false>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
+    }
     if (hook && !bound) hook->after(KIND_RUNSK_KERNEL, s);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
     if (probe) {
