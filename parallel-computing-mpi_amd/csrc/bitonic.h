@@ -485,6 +485,123 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
     }
 }
 
+// The SORT tile's top levels as merge levels.  MISORT_SORT_MERGE (u32) /
+// MISORT_SORT_MERGE_U64 = F: levels 1..F-1 run as the bitonic network
+// (registers, DPP, wave-local LDS phases), leaving sorted runs of 2^(F-1) keys
+// (F <= 12: a run lies inside one wave's 2^11 keys); the runs are laid out
+// plainly in LDS with sentinels after each and merged pairwise in levels
+// F..LT by the multi-way pass's in-LDS machinery (lds_merge.h: phased co-rank
+// searches, merge chains), IT outputs per lane -- instead of barrier-separated
+// LDS phases with LT - F + 1 .. LT stages each.  0 = the network for every
+// level.  Measured on one box each (profiles/r04/sortmerge, sortmerge64):
+//   u32 2^14 tile (the default tile from 2^25, see sort_tile_u32): the 2^30
+//   SORT pass 4.31 ms as a network -> 3.61 (F = 12) -> 3.42 (F = 11) ->
+//   3.60 (F = 10); the 2^15 tile with F = 12: 5.80 (one workgroup per CU).
+//   u64 2^13 tile at 2^29: 5.57 ms -> 5.05 (F = 12) -> 4.74 (11) -> 4.73 (10)
+//   on the persistent grid, 4.43 (12) / 4.32 (10) / 4.31 (9) one tile per
+//   workgroup, 8.4 (8: 88 KiB of LDS, one workgroup per CU).
+// The merge-level tiles run one tile per workgroup: the merge keeps IT more
+// keys per lane live than the network, and the persistent grid's prefetch
+// measured slower.
+#ifndef MISORT_SORT_MERGE
+#define MISORT_SORT_MERGE 11
+#endif
+#ifndef MISORT_SORT_MERGE_U64
+#define MISORT_SORT_MERGE_U64 10
+#endif
+// Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
+// (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
+// (4) and stores what it has -- the differences price each phase.
+#ifndef MISORT_SORT_STOP
+#define MISORT_SORT_STOP 0
+#endif
+template <typename KEY, int LT, int F>
+struct SortMergeShape {
+    static_assert(F >= 7 && F <= 12 && F <= LT, "merge levels from runs of 64 .. 2^11 keys");
+    static constexpr int NT = 1 << (LT - 5);  // 32 keys per lane
+    static constexpr int K = 1 << (LT - F + 1), LKS = LT - F + 1, RUN = 1 << (F - 1);
+    static constexpr int CH = sizeof(KEY) == 4 ? 1 : 0;  // two-key chains for u32, one key per read for u64
+    // odd outputs per lane (the lanes' diagonals on distinct banks), the
+    // smallest >= 33 whose level layouts fit: 2^LT keys + per pair G + QA gap
+    static constexpr int fit(int it) {
+        return (1 << LT) + (K / 2) * (2 * it + (CH == 1 ? 2 : 1)) <= NT * it ? it : fit(it + 2);
+    }
+    static constexpr int IT = fit(33);
+    static constexpr int RN = CH == 1 ? IT + 1 : IT;  // the two-key chain merges an even count
+    static constexpr int G = RN + 1;                   // sentinels after each sequence (a chain reads <= RN past it)
+    static constexpr int QA = IT;                      // pairs start at lane boundaries
+    static constexpr int MAXR = 1 << (LT - 1);         // a last-level pair: two runs of 2^(LT-1)
+    static constexpr int GS = G;
+    static constexpr int WORDS = NT * IT + G + 8;  // the level layouts (>= K runs of RUN + GS)
+    static_assert(K * (RUN + GS) <= WORDS && (1 << LT) + (K / 2) * (G + QA) <= NT * IT, "SORT merge layout");
+};
+
+// Levels F..LT of a tile whose runs of 2^(F-1) keys are sorted in the padded
+// layout (pad(v)): lane l of wave w moves keys w * 2^11 + 64c + l to the plain
+// layout (run q at q * (RUN + GS), GS sentinels after it; consecutive lanes,
+// consecutive words), the runs merge in LDS, and lane t's outputs [t * IT,
+// t * IT + IT) go back to LDS in plain order.  Ends with a barrier.
+template <typename KEY, int LT, int F>
+__device__ __forceinline__ void tile_merge_top(KEY* s, int t) {
+    typedef SortMergeShape<KEY, LT, F> MS;
+    const int w = t >> 6, l = t & 63;
+    KEY y[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) y[c] = s[pad((w << 11) + (c << 6) + l)];
+    lds_barrier();  // LDS-only hand-offs: a persistent tile's prefetch stays in flight
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+        const int v = (w << 11) + (c << 6) + l;
+        s[(v >> (F - 1)) * (MS::RUN + MS::GS) + (v & (MS::RUN - 1))] = y[c];
+    }
+    for (int e = t; e < MS::K * MS::GS; e += MS::NT) {
+        const int q = e / MS::GS;
+        s[q * (MS::RUN + MS::GS) + MS::RUN + (e - q * MS::GS)] = KMAX<KEY>;
+    }
+    lds_barrier();
+    int st[MS::K], ln[MS::K];
+#pragma unroll
+    for (int q = 0; q < MS::K; ++q) {
+        st[q] = q * (MS::RUN + MS::GS);
+        ln[q] = MS::RUN;
+    }
+    KEY r[MS::RN];
+    int ex = 0;
+    lds_merge_levels<KEY, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
+    if (t * MS::IT < (1 << LT)) {
+#pragma unroll
+        for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
+    }
+    lds_barrier();
+}
+
+// LDS (plain layout) -> 16-byte vectors -> HBM, and the first multi-way
+// pass's fences (final_store for the merge-level tile).
+template <typename K, int LT>
+__device__ __forceinline__ void final_store_plain(const K* s, K* out, int64_t tile, int64_t n, bool full, int t,
+                                                  void* fence, int flk) {
+    typedef TileGeo<K, LT> G;
+#pragma unroll
+    for (int k = 0; k < G::LOADS; ++k) {
+        const int e = place<K, LT>(k, t);
+        const typename KT<K>::vec v = *reinterpret_cast<const typename KT<K>::vec*>(s + e);
+        K x[G::V];
+#pragma unroll
+        for (int j = 0; j < G::V; ++j) x[j] = v[j];
+        store_slot<K, LT>(out, tile, n, full, e, x);
+        constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
+        const int64_t gi = (tile << LT) + e;
+        if (fence && (e & FGM) == 0 && gi < n) {
+            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
+                                 (uint32_t)(e >> MERGEK_FENCE_LOG2);
+            if constexpr (sizeof(K) == 4)
+                ((uint64_t*)fence)[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
+            else
+                ((unsigned __int128*)fence)[gi >> MERGEK_FENCE_LOG2] = ((unsigned __int128)x[0] << 64) | tag;
+        }
+    }
+}
+
 // The SORT tile for u64 (and f64, ORD: mapped to ordered u64 on load) keys:
 // levels 1..5 on 32 consecutive keys per lane in registers, 6..LT in 5-bit LDS
 // phases (wave-local ones without a workgroup barrier).  PERSIST: the grid is
@@ -494,7 +611,13 @@ template <typename K, int LT, bool ORD, bool PERSIST>
 __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_sort_tile(
     const K* in, K* out, int64_t n, int64_t ntiles, void* fence, int flk) {
     typedef TileGeo<K, LT> G;
-    __shared__ K s[lds_words(G::T)];
+    // MISORT_SORT_MERGE_U64 = F: levels F..LT as in-LDS merge levels
+    constexpr int MF = sizeof(K) == 8 && MISORT_SORT_TOP_U64 >= LT ? MISORT_SORT_MERGE_U64 : 0;
+    typedef SortMergeShape<K, LT, MF ? MF : 12> MS;
+    // MERGE: 2 keys below the tile (a co-rank probe may read index -1; 16-byte alignment)
+    constexpr int WORDS = MF && MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T);
+    __shared__ __attribute__((aligned(16))) K sbuf[WORDS + (MF ? 2 : 0)];
+    K* s = MF ? sbuf + 2 : sbuf;
     const int t = threadIdx.x;
     K pre[G::LOADS][G::V];
     int64_t tile = blockIdx.x;
@@ -527,8 +650,14 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
         }
         if constexpr (MISORT_SORT_WAVE_SYNC) wave_sync();  // level 6 stays inside the wave
         else __syncthreads();
-        sort_levels_w<K, 6, (sizeof(K) == 8 && MISORT_SORT_TOP_U64 < LT ? MISORT_SORT_TOP_U64 : LT)>(s, t);
-        final_store<K, LT>(s, out, tile, n, full, t, fence, flk);
+        if constexpr (MF > 0) {
+            sort_levels_w<K, 6, MF - 1>(s, t);
+            tile_merge_top<K, LT, MF>(s, t);
+            final_store_plain<K, LT>(s, out, tile, n, full, t, fence, flk);
+        } else {
+            sort_levels_w<K, 6, (sizeof(K) == 8 && MISORT_SORT_TOP_U64 < LT ? MISORT_SORT_TOP_U64 : LT)>(s, t);
+            final_store<K, LT>(s, out, tile, n, full, t, fence, flk);
+        }
         __syncthreads();
         if constexpr (!PERSIST) break;
     }
@@ -559,7 +688,8 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
     typedef TileGeo<K, LT> G;
     static int64_t cap = 0;  // resident workgroups
     const int64_t ntiles = (n + G::T - 1) >> LT;
-    const bool persist = plan_knobs().persist_sort((int)sizeof(K));
+    // the merge-level tile runs one tile per workgroup (see MISORT_SORT_MERGE)
+    const bool persist = !(sizeof(K) == 8 && MISORT_SORT_MERGE_U64 > 0) && plan_knobs().persist_sort((int)sizeof(K));
     if (persist && cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;
         (void)hipGetDevice(&dev);
@@ -604,62 +734,6 @@ __device__ __forceinline__ void sort_fetch(uint32_t (*pre)[4], const uint32_t* i
     }
 }
 
-// The u32 SORT tile's top levels as merge levels (MISORT_SORT_MERGE = 12):
-// levels 1..11 run as the bitonic network (registers, DPP, wave-local LDS
-// phases: each wave then holds a sorted run of 2^11 keys), then the 16 runs
-// are laid out plainly in LDS with sentinels after each and merged pairwise in
-// four levels by the multi-way pass's in-LDS machinery (lds_merge.h: phased
-// co-rank searches, two-key chains), 33 outputs per lane -- instead of levels
-// 12..LT as barrier-separated LDS phases (1.83 of the 2^15 pass's 4.8 ms).
-// The merge keeps 34 more registers per lane live than the network, so the
-// tile runs one workgroup per tile (no next-tile prefetch in registers: it
-// would spill); with MISORT_SORT_LT_U32 = 14 two workgroups per CU overlap
-// each other's loads.  0 = the bitonic network for every level.
-#ifndef MISORT_SORT_MERGE
-#define MISORT_SORT_MERGE 12
-#endif
-// Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
-// (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
-// (4) and stores what it has -- the differences price each phase.
-#ifndef MISORT_SORT_STOP
-#define MISORT_SORT_STOP 0
-#endif
-template <int LT>
-struct SortMergeShape {
-    static constexpr int K = 1 << (LT - 11), LKS = LT - 11, NT = 1 << (LT - 5);  // 2^11-key runs, 32 keys per lane
-    static constexpr int IT = 33;       // odd: lanes' diagonals on distinct banks; NT x 33 >= 2^LT + pair gaps
-    static constexpr int RN = IT + 1;   // the two-key chain merges an even count
-    static constexpr int G = RN + 1;    // sentinels after each sequence (a chain reads <= RN past it)
-    static constexpr int QA = IT;       // pairs start at lane boundaries
-    static constexpr int CH = 1;
-    static constexpr int MAXR = 1 << (LT - 1);  // a last-level pair: two runs of 2^(LT-1)
-    static constexpr int RUN = 1 << 11, GS = G;
-    static constexpr int WORDS = NT * IT + G + 8;  // the level layouts (>= K runs of RUN + GS)
-    static_assert(K * (RUN + GS) <= WORDS && (1 << LT) + (K / 2) * (G + QA) <= NT * IT, "SORT merge layout");
-};
-
-// LDS (plain layout) -> 16-byte vectors -> HBM, and the first multi-way
-// pass's fences (final_store for the merge-level tile).
-template <int LT>
-__device__ __forceinline__ void final_store_plain(const uint32_t* s, uint32_t* out, int64_t tile, int64_t n, bool full,
-                                                  int t, uint64_t* fence, int flk) {
-    typedef TileGeo<uint32_t, LT> G;
-#pragma unroll
-    for (int k = 0; k < G::LOADS; ++k) {
-        const int e = place<uint32_t, LT>(k, t);
-        const KT<uint32_t>::vec v = *reinterpret_cast<const KT<uint32_t>::vec*>(s + e);
-        uint32_t x[4] = {v[0], v[1], v[2], v[3]};
-        store_slot<uint32_t, LT>(out, tile, n, full, e, x);
-        constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
-        const int64_t gi = (tile << LT) + e;
-        if (fence && (e & FGM) == 0 && gi < n) {
-            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
-                                 (uint32_t)(e >> MERGEK_FENCE_LOG2);
-            fence[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
-        }
-    }
-}
-
 // 2^15 tile: 1024 lanes, one workgroup per CU; 2^14: 512 lanes, two
 // workgroups per CU (4 waves per SIMD: 128 VGPRs per lane)
 template <int LT, bool PERSIST, bool FULL>
@@ -670,8 +744,9 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
     static_assert(LT == 14 || LT == 15, "u32 SORT tiles");
     constexpr int WL = MISORT_WAVE_LEVELS;
     static_assert(G::LOADS == 8 && (G::NT == 1024 || G::NT == 512) && WL >= 5 && WL <= 10, "u32 SORT tile shape");
-    constexpr bool MERGE = MISORT_SORT_MERGE == 12 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
-    typedef SortMergeShape<LT> MS;
+    constexpr int MF = MISORT_SORT_MERGE;  // first merged level (0: none)
+    constexpr bool MERGE = MF > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
+    typedef SortMergeShape<K, LT, MERGE ? MF : 12> MS;
     // MERGE: 4 words below the tile (a co-rank probe may read index -1)
     __shared__ __attribute__((aligned(16))) K sbuf[(MERGE ? (MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T)) + 4
                                                           : lds_words(G::T))];
@@ -718,39 +793,13 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < ntiles) sort_fetch<LT, FULL>(pre, in, nxt, n, t);
         if constexpr (MERGE) {
-            if constexpr (STOP == 0 || STOP >= 3) sort_levels_w<K, WL + 1, 11>(s, t);
-            // wave w's sorted run (keys w * 2^11 ...) -> plain layout at
-            // w * (RUN + GS), then GS sentinels; lane l moves keys 64c + l
-            // (consecutive lanes, consecutive words: no bank conflicts)
-            const int w = t >> 6, l = t & 63;
-            if constexpr (STOP == 0 || STOP >= 4) {
-                uint32_t y[32];
-#pragma unroll
-                for (int c = 0; c < 32; ++c) y[c] = s[pad((w << 11) + (c << 6) + l)];
+            if constexpr (STOP == 0 || STOP >= 3) sort_levels_w<K, WL + 1, (MERGE ? MF : 12) - 1>(s, t);
+            if constexpr (STOP == 0) {
+                tile_merge_top<K, LT, (MERGE ? MF : 12)>(s, t);
+            } else {
                 __syncthreads();
-                const int b0 = w * (MS::RUN + MS::GS);
-#pragma unroll
-                for (int c = 0; c < 32; ++c) s[b0 + (c << 6) + l] = y[c];
-                if (l < MS::GS) s[b0 + MS::RUN + l] = 0xFFFFFFFFu;
             }
-            __syncthreads();
-            int st[MS::K], ln[MS::K];
-#pragma unroll
-            for (int q = 0; q < MS::K; ++q) {
-                st[q] = q * (MS::RUN + MS::GS);
-                ln[q] = MS::RUN;
-            }
-            uint32_t r[MS::RN];
-            int ex = 0;
-            if constexpr (STOP == 0) lds_merge_levels<uint32_t, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
-            // the merged tile: lane t's outputs [33 t, 33 t + 33) back to LDS
-            // (the last level's reads are done), then out as 16-byte vectors
-            if (STOP == 0 && t * MS::IT < G::T) {
-#pragma unroll
-                for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
-            }
-            __syncthreads();
-            final_store_plain<LT>(s, out, tile, n, FULL, t, fence, flk);
+            final_store_plain<K, LT>(s, out, tile, n, FULL, t, fence, flk);
         } else {
             sort_levels_w<K, WL + 1, (MISORT_SORT_TOP < LT ? MISORT_SORT_TOP : LT)>(s, t);
             final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
@@ -767,7 +816,7 @@ void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s
                      int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     constexpr int NT = TileGeo<uint32_t, LT>::NT;
     // the merge-level tile runs one workgroup per tile (see MISORT_SORT_MERGE)
-    constexpr bool MERGE = MISORT_SORT_MERGE == 12 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
+    constexpr bool MERGE = MISORT_SORT_MERGE > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
     static int64_t cap = 0;
     const int64_t nfull = n >> LT;
     const bool persist = !MERGE && plan_knobs().persist_sort(4);
