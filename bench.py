@@ -525,8 +525,10 @@ def main(argv=None):
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        local_algo = ("bitonic LDS tiles (2^15 u32 / 2^13 u64 keys), then multi-way merge passes: 3-4 "
-                      "merge levels per HBM pass (8/16-way, runsk.hip; u64 with 128-bit fences) "
+        tile = misort.plan(loc, key_bytes)[0][1] + 1
+        local_algo = (f"SORT tiles of 2^{tile} keys in LDS (bitonic network, top levels as in-LDS merge "
+                      "levels), then multi-way merge passes of up to 4 merge levels per HBM pass (16-way, "
+                      "runsk.hip; u32 with 64-bit fences, u64 with 128-bit) "
                       "(the reference's local std::sort, psort.cc:175)")
         out = {
             "metric": METRIC,
