@@ -134,12 +134,23 @@ struct KTr<uint32_t> {
 static_assert(KTr<uint32_t>::NT == 256 || KTr<uint32_t>::NT == 384 || KTr<uint32_t>::NT == 512 ||
                   KTr<uint32_t>::NT == 1024,
               "chunk workgroup");
+// The u64 chunk shape: 18 outputs per lane and the largest capacity whose
+// level layout fits 512 x 18 slots (CAP + 8 (G + QA) <= 9216): 8832 keys
+// (69 fences of 128) instead of 8192 measured 2^29 u64 35.4 -> 36.5-36.7
+// Gkeys/s, k_mergek 2.46 -> 2.33 ms per pass, 2^26 +2.2 %; 9216 keys at 20 per
+// lane was slower (profiles/r04/chunk64).  Build-time probes: tools/build_variant.sh.
+#ifndef MISORT_MK_IT64
+#define MISORT_MK_IT64 18
+#endif
+#ifndef MISORT_MK_CAP64
+#define MISORT_MK_CAP64 8832
+#endif
 template <>
 struct KTr<uint64_t> {
     typedef u128 F;
     static constexpr int NT = 512;
-    static constexpr int IT = 18;
-    static constexpr int CAP = 8192;     // 64 KiB of keys: two tiles per CU, 4 waves per SIMD
+    static constexpr int IT = MISORT_MK_IT64;
+    static constexpr int CAP = MISORT_MK_CAP64;  // 69 KiB of keys: two tiles per CU, 4 waves per SIMD
     static constexpr int WG_PER_CU = 2;
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
