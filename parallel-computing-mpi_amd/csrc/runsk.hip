@@ -121,7 +121,9 @@ struct KTr<uint32_t> {
     typedef uint64_t F;
     static constexpr int NT = MISORT_MK_NT;
     static constexpr int IT = MISORT_MK_IT ? MISORT_MK_IT : NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
-    static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT >= 512 ? 16 * NT : 8192;  // 8192 at 512 lanes
+    // 8960 at 512 lanes: the largest the 18-output level layout fits (CAP + 4 (G + QA) <= 9216; 8192
+    // before: 2^24 +1.5 %, 2^28 +0.8 %, profiles/r04/chunk32)
+    static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT == 512 ? 8960 : NT > 512 ? 16 * NT : 8192;
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     // the chunk shape of a pass of lk levels
     static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
