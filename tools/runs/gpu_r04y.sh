@@ -1,0 +1,7 @@
+# Round 4, call Y: the HEAD measurement set (call X's script), then in-wave
+# levels up to 9 / 10 (MISORT_WAVE_LEVELS variants) against the default 8.
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; cd "$R"
+bash tools/runs/gpu_r04x.sh || exit $?
+TESTS="tests/test_gpu_runs.py tests/test_gpu_parity.py" VARIANTS="wl10" ROUNDS=0 OUTDIR=r04y bash tools/gpu_abv.sh || exit $?
+SKIP_TESTS=1 VARIANTS="base wl9 wl10" DTYPES=u32 LOGNS="30 28 24" ROUNDS=2 OUTDIR=r04y bash tools/gpu_abv.sh
