@@ -509,6 +509,11 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_MERGE_U64
 #define MISORT_SORT_MERGE_U64 10
 #endif
+// Probe (tools/build_variant.sh): the merge-level u32 tile on the persistent
+// grid with the next tile's loads in flight.
+#ifndef MISORT_SORT_MERGE_PERSIST
+#define MISORT_SORT_MERGE_PERSIST 0
+#endif
 // Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
 // (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
 // (4) and stores what it has -- the differences price each phase.
@@ -768,7 +773,8 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
 #pragma unroll
             for (int j = 0; j < G::V; ++j) s[pad(e + j)] = pre[k][j];
         }
-        __syncthreads();
+        if constexpr (MERGE) lds_barrier();  // no wait for the previous tile's stores
+        else __syncthreads();
         constexpr int STOP = MERGE ? MISORT_SORT_STOP : 0;
         if constexpr (STOP == 0 || STOP >= 2) {
             uint32_t x[32];
@@ -805,7 +811,9 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
             final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
         }
         if constexpr (!PERSIST) break;
-        __syncthreads();
+        // LDS reuse only: the merge tile keeps the next tile's loads in flight
+        if constexpr (MERGE) lds_barrier();
+        else __syncthreads();
     }
 }
 
@@ -819,11 +827,12 @@ void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s
     constexpr bool MERGE = MISORT_SORT_MERGE > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
     static int64_t cap = 0;
     const int64_t nfull = n >> LT;
-    const bool persist = !MERGE && plan_knobs().persist_sort(4);
+    constexpr bool MP = MERGE && MISORT_SORT_MERGE_PERSIST;
+    const bool persist = (!MERGE || MP) && plan_knobs().persist_sort(4);
     const bool tail = (nfull << LT) < n;
     if (nfull > 0) {
         hipEvent_t b = tail ? nullptr : eb;
-        if constexpr (!MERGE) {
+        if constexpr (!MERGE || MP) {
             if (persist) {
                 if (cap == 0) {
                     int per_cu = 0, cus = 0, dev = 0;
