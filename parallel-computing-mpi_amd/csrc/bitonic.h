@@ -509,11 +509,6 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_MERGE_U64
 #define MISORT_SORT_MERGE_U64 10
 #endif
-// Probe (tools/build_variant.sh): the merge-level u32 tile on the persistent
-// grid with the next tile's loads in flight.
-#ifndef MISORT_SORT_MERGE_PERSIST
-#define MISORT_SORT_MERGE_PERSIST 0
-#endif
 // Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
 // (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
 // (4) and stores what it has -- the differences price each phase.
@@ -827,12 +822,13 @@ void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s
     constexpr bool MERGE = MISORT_SORT_MERGE > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
     static int64_t cap = 0;
     const int64_t nfull = n >> LT;
-    constexpr bool MP = MERGE && MISORT_SORT_MERGE_PERSIST;
-    const bool persist = (!MERGE || MP) && plan_knobs().persist_sort(4);
+    // (on the persistent grid with the next tile's loads in flight it spills
+    // 16 VGPRs and ran 3.45 -> 4.15 ms at 2^30; profiles/r04/sortwave)
+    const bool persist = !MERGE && plan_knobs().persist_sort(4);
     const bool tail = (nfull << LT) < n;
     if (nfull > 0) {
         hipEvent_t b = tail ? nullptr : eb;
-        if constexpr (!MERGE || MP) {
+        if constexpr (!MERGE) {
             if (persist) {
                 if (cap == 0) {
                     int per_cu = 0, cus = 0, dev = 0;
