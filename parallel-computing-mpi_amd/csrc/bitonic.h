@@ -510,8 +510,8 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #define MISORT_SORT_MERGE_U64 10
 #endif
 // Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
-// (1), the register/DPP levels (2), the LDS levels to 11 (3) or the relayout
-// (4) and stores what it has -- the differences price each phase.
+// (1), the register/DPP levels (2) or the LDS levels below the merged ones
+// (3) and stores what it has -- the differences price each phase.
 #ifndef MISORT_SORT_STOP
 #define MISORT_SORT_STOP 0
 #endif

@@ -132,7 +132,7 @@ int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
 constexpr int MERGEK_FENCE_LOG2 = MISORT_MK_FG_LOG2;
 // log2 keys of the u32 SORT tiles (bitonic.h).  15: 1024 lanes, one
 // workgroup per CU, all 15 levels as the bitonic network.  14: 512 lanes, two
-// workgroups per CU, levels 12..14 as in-LDS merge levels (MISORT_SORT_MERGE).
+// workgroups per CU, levels 11..14 as in-LDS merge levels (MISORT_SORT_MERGE).
 // The plan picks per size (sort_tile_u32); u32 multi-way passes take runs of
 // 2^14 and up.
 constexpr int SORT_LT_U32 = 15, SORT_LT_MERGE = 14;
