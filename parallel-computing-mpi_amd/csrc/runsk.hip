@@ -90,6 +90,10 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
 #endif
+// k_mergek stages a chunk whose output shift is even with pair writes.
+#ifndef MISORT_MK_PAIRSTAGE
+#define MISORT_MK_PAIRSTAGE 1
+#endif
 // The in-LDS merge levels of k_mergek: 0 = one key per LDS read (merge_chain),
 // 1 / 2 = two keys per read (merge_chain_blk; 1: ds_read2_b32 / ds_read2_b64,
 // 2: one unaligned ds_read_b64 / ds_read_b128).  Measured at 2^30 u32
@@ -926,9 +930,16 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
     const int sh = (int)(out0 & (VK - 1));
     if (pos < len) {
         KEY* q = s + sh + pos - ex;
+        if (S::CH != 3 && IT % 2 == 0 && MISORT_MK_PAIRSTAGE && (sh & 1) == 0) {
+            // even shift (uniform per chunk): aligned pairs, one 8-byte (u64:
+            // 16-byte) write per two keys instead of one write per key
 #pragma unroll
-        for (int k = 0; k < RN; ++k)
-            if (k >= ex && k < ex + IT) q[k] = r[k];
+            for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(q + j) = kvec2<KEY>{r[j], r[j + 1]};
+        } else {
+#pragma unroll
+            for (int k = 0; k < RN; ++k)
+                if (k >= ex && k < ex + IT) q[k] = r[k];
+        }
     }
     lds_barrier();
     const int nv = (sh + len + VK - 1) / VK;
