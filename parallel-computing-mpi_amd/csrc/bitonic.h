@@ -509,6 +509,11 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_MERGE_U64
 #define MISORT_SORT_MERGE_U64 10
 #endif
+// The u32 merge-level tile's smallest outputs per lane (even: aligned pair
+// writes; 33 = the odd layout measured first).
+#ifndef MISORT_SORT_IT0
+#define MISORT_SORT_IT0 34
+#endif
 // Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
 // (1), the register/DPP levels (2) or the LDS levels below the merged ones
 // (3) and stores what it has -- the differences price each phase.
@@ -521,13 +526,17 @@ struct SortMergeShape {
     static constexpr int NT = 1 << (LT - 5);  // 32 keys per lane
     static constexpr int K = 1 << (LT - F + 1), LKS = LT - F + 1, RUN = 1 << (F - 1);
     static constexpr int CH = sizeof(KEY) == 4 ? 1 : 0;  // two-key chains for u32, one key per read for u64
-    // odd outputs per lane (the lanes' diagonals on distinct banks), the
-    // smallest >= 33 whose level layouts fit: 2^LT keys + per pair G + QA gap
+    // outputs per lane: the smallest count from IT0 up (step 2) whose level
+    // layouts fit: 2^LT keys + per pair G + QA gap.  u32: even (IT0 = 34),
+    // so every level writes aligned pairs; u64: odd (33: lanes' diagonals on
+    // distinct banks; a pair of u64 keys is a 16-byte write, no cheaper than two)
+    static constexpr int IT0 = CH == 1 ? MISORT_SORT_IT0 : 33;
+    static constexpr int rn(int it) { return CH == 1 ? (it + 1) & ~1 : it; }
     static constexpr int fit(int it) {
-        return (1 << LT) + (K / 2) * (2 * it + (CH == 1 ? 2 : 1)) <= NT * it ? it : fit(it + 2);
+        return (1 << LT) + (K / 2) * (rn(it) + 1 + it) <= NT * it ? it : fit(it + 2);
     }
-    static constexpr int IT = fit(33);
-    static constexpr int RN = CH == 1 ? IT + 1 : IT;  // the two-key chain merges an even count
+    static constexpr int IT = fit(IT0);
+    static constexpr int RN = rn(IT);                  // the two-key chain merges an even count
     static constexpr int G = RN + 1;                   // sentinels after each sequence (a chain reads <= RN past it)
     static constexpr int QA = IT;                      // pairs start at lane boundaries
     static constexpr int MAXR = 1 << (LT - 1);         // a last-level pair: two runs of 2^(LT-1)
@@ -569,8 +578,13 @@ __device__ __forceinline__ void tile_merge_top(KEY* s, int t) {
     int ex = 0;
     lds_merge_levels<KEY, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
     if (t * MS::IT < (1 << LT)) {
+        if constexpr (MS::CH == 1 && MS::IT % 2 == 0) {
 #pragma unroll
-        for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
+            for (int j = 0; j < MS::IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(s + t * MS::IT + j) = kvec2<KEY>{r[j], r[j + 1]};
+        } else {
+#pragma unroll
+            for (int j = 0; j < MS::IT; ++j) s[t * MS::IT + j] = r[j];
+        }
     }
     lds_barrier();
 }
