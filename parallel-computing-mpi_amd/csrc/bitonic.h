@@ -900,18 +900,24 @@ inline std::vector<Pass> plan_uncached(int k, int key_bytes, int LT) {
     return ps;
 }
 
-// The u32 SORT tile for 2^k-key blocks: the 2^14 merge-level tile where it
-// adds no multi-way pass, from 2^25 up; the 2^15 network tile otherwise.  One
-// box, 2 x 10 sorts each (profiles/r04/sortmerge): 2^30 (16 levels after the
-// 2^14 tile, 15 after 2^15: four passes either way) SORT pass 4.97 -> 3.61 ms,
-// 73.0 -> 76.8 Gkeys/s; 2^28 +4 %; 2^24 (4,3,3 vs 3,3,3 levels) -2 %; 2^27
-// would take a fifth pass.
+// The u32 SORT tile for 2^k-key blocks: the 2^14 merge-level tile, except
+// for tiny sorts (k <= 15) and below 2^25 where only its plan has a 16-way
+// pass (a 16-way pass over a small sort costs more than the faster tile
+// saves).  Measured at HEAD, one box, 30 sorts per point (profiles/r04/tile):
+// 2^14 vs 2^15 tiles 2^20 +11 %, 2^22 +2 %, 2^23 +4 %, 2^24 -4 % (4,3,3 vs
+// 3,3,3 levels), 2^25 +1 %, 2^26 +3 %, 2^27 +4 % (four passes against three),
+// 2^29 +5 %; 2^18 and 2^21 equal.
 inline int sort_tile_u32(int k) {
     const int knob = plan_knobs().sort_tile_u32;
     if (knob == SORT_LT_MERGE || knob == SORT_LT_U32) return knob;
-    if (k < 25) return SORT_LT_U32;
-    return plan_uncached(k, 4, SORT_LT_MERGE).size() <= plan_uncached(k, 4, SORT_LT_U32).size() ? SORT_LT_MERGE
-                                                                                              : SORT_LT_U32;
+    if (k <= SORT_LT_U32) return SORT_LT_U32;
+    if (k >= 25) return SORT_LT_MERGE;
+    auto has16 = [k](int lt) {
+        for (const Pass& p : plan_uncached(k, 4, lt))
+            if (p.kind == KIND_RUNSK && p.R == 4) return true;
+        return false;
+    };
+    return has16(SORT_LT_MERGE) && !has16(SORT_LT_U32) ? SORT_LT_U32 : SORT_LT_MERGE;
 }
 
 // Cached per (key type, ceil_log2(n)): the knobs are read once per process.

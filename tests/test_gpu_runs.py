@@ -197,10 +197,12 @@ ctx.close()
     (4, {"MISORT_MULTIWAY": "2"}, (1 << 22) + 4099),
     (4, {"MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),  # chained 8-way passes, u64 fence merges
     (4, {}, (1 << 27) + 777),  # the default: 2^14 tiles, four 16-way passes
-    (4, {}, (1 << 26) + 777),  # 2^15 tiles (2^14 ones would add a pass): three 16-way passes
+    (4, {}, (1 << 26) + 777),  # 2^14 tiles, 4 + 3 + 3 + 3 levels
+    (4, {}, (1 << 23) + 5),  # 2^15 tiles (2^14 ones would need a 16-way pass): three 8-way passes
+    (4, {}, (1 << 17) + 9),  # 2^15 tiles, one 8-way pass
     (4, {}, (1 << 25) + 3),  # 2^14 merge-level tiles, 4 + 4 + 4 levels
     (4, {"MISORT_SORT_TILE_U32": "15"}, (1 << 25) + 3),  # 2^15 tiles, 4 + 4 + 3 levels
-    (4, {"MISORT_SORT_TILE_U32": "14"}, (1 << 22) + 4099),  # 2^14 tiles at a size that defaults to 2^15
+    (4, {"MISORT_SORT_TILE_U32": "14"}, (1 << 23) + 4099),  # 2^14 tiles at a size that defaults to 2^15
     (4, {"MISORT_SORT_TILE_U32": "14"}, (1 << 14) + 1),  # one level past the 2^14 tile: a 2-way pass
     (4, {"MISORT_SORT_TILE_U32": "14"}, 3 * (1 << 14) - 5),  # a full tile + a partial one
     (4, {"MISORT_SORT_TILE_U32": "14", "MISORT_MULTIWAY": "3"}, (1 << 24) + 12345),
@@ -227,8 +229,8 @@ ctx.close()
 def test_full_sort_merge_passes(kb, env, n):
     """The whole local sort (SORT tile, then merge passes) under the planner
     knobs, against np.sort; the plan has the fewest multi-way passes for the
-    levels past the tile (u32: 2^14 keys from 2^25 where that adds no pass,
-    else 2^15; u64: 2^13)."""
+    levels past the tile (u32: 2^14 or 2^15 keys by size, sort_tile_u32;
+    u64: 2^13)."""
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd"), str(n),
                         str(kb)], env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -49,6 +49,26 @@ def replay(keys, plan):
     return x[:n]
 
 
+def widths(L, cap=4):
+    """plan_uncached's multi-way pass widths for L levels (fewest passes of
+    <= cap levels, the larger ones first; one level alone is a 2-way pass)."""
+    if L < 2:
+        return []
+    np_ = -(-L // cap)
+    return [L // np_ + (1 if i < L % np_ else 0) for i in range(np_)]
+
+
+def expected_tile_u32(k):
+    """sort_tile_u32 (bitonic.h): the 2^14 merge-level tile except for tiny
+    sorts and, below 2^25, where only its plan has a 16-way pass."""
+    if k <= 15:
+        return 15
+    if k >= 25:
+        return 14
+    has16 = lambda lt: 4 in widths(min(k, 30) - lt)
+    return 15 if has16(14) and not has16(15) else 14
+
+
 SIZES = [1, 2, 31, 1000, (1 << 13) + 1, (1 << 15) - 3, 1 << 15, (1 << 15) + 1, 1 << 16, 100003, 1 << 18,
          (1 << 20) - 7, 1 << 23, 1 << 24, 1 << 28, (1 << 29) - 3, 1 << 30, 1 << 31]
 
@@ -61,9 +81,7 @@ def test_plan_covers_the_levels(n, key_bytes):
     assert p[0][0] == KIND_SORT
     lt = p[0][1] + 1
     k = ceil_log2(n)
-    assert lt in ((14, 15) if key_bytes == 4 else (13,))
-    if key_bytes == 4 and lt == 14:  # only from 2^25, and only where it adds no merge pass
-        assert k >= 25 and k != 27
+    assert lt == (expected_tile_u32(k) if key_bytes == 4 else 13)
     assert merge_levels(p) == list(range(lt, k))
     lwk_max = 30 if key_bytes == 4 else 29  # 32-bit row offsets of a multi-way group
     for kind, hi, r, _ in p[1:]:
@@ -80,22 +98,24 @@ def test_plan_pass_counts():
                                                 (KIND_RUNSK, 26, 4)]
     # the fewest passes of at most four levels (16-way) at every size
     # (profiles/r04/mw: faster than 8-way passes from 2^26 to 2^31); the
-    # 2^14 tile from 2^25 where it adds no pass (profiles/r04/sortmerge)
+    # 2^14 tile (profiles/r04/tile: 2^27 takes four passes on it and is 4 %
+    # faster than three on 2^15 tiles)
     assert [q[2] for q in misort.plan(1 << 28, 4)[1:]] == [4, 4, 3, 3]
     assert [q[2] for q in misort.plan(1 << 29, 4)[1:]] == [4, 4, 4, 3]
-    assert [q[1] for q in misort.plan(1 << 27, 4)] == [14, 15, 19, 23]  # 2^15 tiles: 2^14 ones would add a pass
-    assert [q[2] for q in misort.plan(1 << 27, 4)[1:]] == [4, 4, 4]
+    assert [q[1] for q in misort.plan(1 << 27, 4)] == [13, 14, 18, 21, 24]
     assert [q[2] for q in misort.plan(1 << 25, 4)[1:]] == [4, 4, 3]
     assert [q[2] for q in misort.plan(1 << 26, 4)[1:]] == [4, 4, 4]
-    assert misort.plan(1 << 24, 4)[0][1] == 14  # below 2^25: 2^15 tiles
+    # 2^24: 2^15 tiles (3,3,3): the 2^14 tile's plan (4,3,3) has a 16-way pass
+    assert misort.plan(1 << 24, 4)[0][1] == 14 and [q[2] for q in misort.plan(1 << 24, 4)[1:]] == [3, 3, 3]
     # 2^31: a multi-way pass may end at 2^30 at most (32-bit row offsets); one 2-way pass after
     assert [q[0] for q in misort.plan(1 << 31, 4)] == [KIND_SORT] + [KIND_RUNSK] * 4 + [KIND_RUNS]
     # small u32 sorts take the merge passes too (round 3: they beat the bitonic
     # network's ROWS/SPAN/MERGE passes at every size, profiles/r03/small_u32)
-    assert [q[0] for q in misort.plan(1 << 23, 4)] == [KIND_SORT] + [KIND_RUNSK] * 2  # 4 + 4 levels
+    assert [q[0] for q in misort.plan(1 << 23, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^14 tiles: 3 x 8-way
     assert [q[0] for q in misort.plan(1 << 24, 4)] == [KIND_SORT] + [KIND_RUNSK] * 3  # 2^24: 3 x 8-way (9 levels)
-    assert [q[0] for q in misort.plan(1 << 16, 4)] == [KIND_SORT, KIND_RUNS]  # one level: 2-way
+    assert [q[0] for q in misort.plan(1 << 16, 4)] == [KIND_SORT, KIND_RUNSK]  # 2^14 tiles, one 4-way pass
     assert [q[0] for q in misort.plan(1 << 15, 4)] == [KIND_SORT]  # one tile
+    assert [q[0] for q in misort.plan(1 << 18, 4)] == [KIND_SORT, KIND_RUNSK]  # 2^15 tiles, one 8-way pass
     # u64: 2^13-key SORT tiles, then 16 levels in four 16-way passes
     # (128-bit fences; 2-way passes would be 1 + 16)
     p29 = misort.plan((1 << 29) - 3, 8)
@@ -161,7 +181,7 @@ def test_sort_tile_knob(tile):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sizes = [(1 << 14) + 1, (1 << 20) + 3, 1 << 27, 1 << 30]
+    sizes = [(1 << 14) + 1, (1 << 18) + 3, 1 << 24, 1 << 27, 1 << 30]
     r = subprocess.run([sys.executable, "-c", PLAN_CHILD, os.path.join(root, "parallel-computing-mpi_amd"),
                         ",".join(map(str, sizes))], env=dict(os.environ, MISORT_SORT_TILE_U32=tile),
                        capture_output=True, text=True, timeout=120)
