@@ -51,7 +51,9 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--logn", type=int, default=30, help="log2 of the total key count")
-    ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
+    ap.add_argument("--dtype", choices=["u32", "u64", "f64"], default="u32",
+                    help="f64: the reference's own key type (psort.cc:565), SplitMix64 top 53 bits as "
+                         "uniform doubles in [0, 1)")
     ap.add_argument("--algo", choices=["bitonic", "sample"], default="bitonic",
                     help="bitonic = psort.cc:167 (the metric); sample = psort.cc:203-375 redesigned")
     ap.add_argument("--no-alt", action="store_true",
@@ -161,8 +163,9 @@ def ref_psort_time(logn, cores):
     return float(m.group(1)), int(errs.group(1)) if errs else None
 
 
-def cpu_baseline(sample_logn, sweep, sweep_logn):
-    """The reference sorter's parallel_bitonic_sort on this host's cores."""
+def cpu_baseline(sample_logn, sweep, sweep_logn, dtype="u32"):
+    """The reference sorter's parallel_bitonic_sort on this host's cores (u32
+    keys carried as doubles, or f64 keys for an f64 workload)."""
     share, why = cpu_share()
     cores = pow2_floor(share)
     model = cpu_model()
@@ -177,12 +180,14 @@ def cpu_baseline(sample_logn, sweep, sweep_logn):
            "cores_why": f"largest power of two <= CPUs available ({why}); psort.cc needs 2^d ranks",
            "cpu": model}
     try:
-        t, errs = ref_keys_time(sample_logn, cores)
+        kd = "f64" if dtype == "f64" else "u32"
+        t, errs = ref_keys_time(sample_logn, cores, kd)
+        what = ("f64 keys (SplitMix64 seed {:#x} top 53 bits as doubles in [0, 1), the bench workload)"
+                if kd == "f64" else "u32 keys (SplitMix64 seed {:#x}, the bench workload) carried as doubles")
         res.update(value=(1 << sample_logn) / t / 1e9, sort_s=t, errors=errs,
-                   sample=(f"2^{sample_logn} u32 keys (SplitMix64 seed {SEED:#x}, the bench workload) "
-                           f"carried as doubles through the reference psort.cc parallel_bitonic_sort "
-                           f"(oracle/_ref harness), mpirun -np {cores}; timed region psort.cc:633-653, "
-                           f"max over ranks"))
+                   sample=(f"2^{sample_logn} {what.format(SEED)} through the reference psort.cc "
+                           f"parallel_bitonic_sort (oracle/_ref harness), mpirun -np {cores}; timed region "
+                           f"psort.cc:633-653, max over ranks"))
     except (RuntimeError, subprocess.TimeoutExpired, OSError, AttributeError) as e:
         sys.stderr.write(f"WARNING cpu baseline failed: {e}\n")
         return port_baseline(min(sample_logn, 24), f"reference run failed: {e}")
@@ -241,6 +246,8 @@ def baseline_config(logn, dtype):
         return f"BASELINE config {({24: 2, 28: 3, 30: 4})[logn]}"
     if dtype == "u64" and logn == 29:
         return "BASELINE config 5's key type and size (N = 2^29, not 2^29 - 3 / - 7)"
+    if dtype == "f64":
+        return "the reference's own key type, psort.cc:565; not a BASELINE config"
     return "not a BASELINE config"
 
 
@@ -331,7 +338,7 @@ def main(argv=None):
         path = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
-                               args.cpu_sweep, args.cpu_sweep_logn)
+                               args.cpu_sweep, args.cpu_sweep_logn, args.dtype)
             fd, path = tempfile.mkstemp(prefix="misort_bench_cpu_", suffix=".json")
             with os.fdopen(fd, "w") as f:
                 json.dump(cpu, f)
@@ -359,7 +366,7 @@ def main(argv=None):
         cpu = load_cpu_json(os.environ.get(CPU_JSON_ENV))
         if cpu is None:
             cpu = cpu_baseline(args.logn if args.cpu_sample_logn is None else args.cpu_sample_logn,
-                               args.cpu_sweep, args.cpu_sweep_logn)
+                               args.cpu_sweep, args.cpu_sweep_logn, args.dtype)
 
     # RCCL logs (its version banner too) go to stderr: stdout is the JSON line
     os.environ.setdefault("NCCL_DEBUG_FILE", "/dev/stderr")
@@ -383,13 +390,29 @@ def main(argv=None):
     sizes = misort.block_sizes(n_total, nranks)
     loc, max_size = sizes[rank], n_total // nranks + 1
     g0 = sum(sizes[:rank])
-    kdt = (torch.uint32 if hasattr(torch, "uint32") else torch.int32) if args.dtype == "u32" else \
-          (torch.uint64 if hasattr(torch, "uint64") else torch.int64)
+    if args.dtype == "f64":
+        kdt = torch.float64
+    elif args.dtype == "u32":
+        kdt = torch.uint32 if hasattr(torch, "uint32") else torch.int32
+    else:
+        kdt = torch.uint64 if hasattr(torch, "uint64") else torch.int64
     key_bytes = 4 if args.dtype == "u32" else 8
+
+    def fill(t, g):
+        if args.dtype == "f64":
+            # SplitMix64 bits -> uniform doubles in [0, 1): the reference's key
+            # type and (pre-skew) distribution, psort.cc:600-609
+            z = torch.empty(t.numel(), dtype=torch.int64, device=t.device)
+            ctx.fill_splitmix(z, SEED, g)
+            t.copy_(((z >> 11) & ((1 << 53) - 1)).to(torch.float64) * 2.0 ** -53)
+            del z
+        else:
+            ctx.fill_splitmix(t, SEED, g)
+
     d_in = torch.empty(max(loc, 1), dtype=kdt, device="cuda")
     d_out = torch.empty_like(d_in)
     stream = torch.cuda.current_stream()
-    ctx.fill_splitmix(d_in[:loc], SEED, g0)
+    fill(d_in[:loc], g0)
     torch.cuda.synchronize()
 
     def barrier():
@@ -483,7 +506,10 @@ def main(argv=None):
             solo = misort.Context(dev)
             a = torch.empty(n_total, dtype=kdt, device="cuda")
             b = torch.empty_like(a)
-            solo.fill_splitmix(a, SEED, 0)
+            if args.dtype == "f64":
+                a.copy_(d_in[:loc]) if nranks == 1 else fill(a, 0)
+            else:
+                solo.fill_splitmix(a, SEED, 0)
             for _ in range(2):
                 solo.parallel_bitonic_sort(a, n_total, n_total, out=b, stream=stream.cuda_stream)
             torch.cuda.synchronize()
@@ -501,7 +527,8 @@ def main(argv=None):
     host_io = None
     if args.host_io:
         # host keys of the same workload; sorted through the pinned staging pipeline
-        h_in = d_in[:loc].cpu().numpy().view(np.uint32 if key_bytes == 4 else np.uint64)
+        h_in = d_in[:loc].cpu().numpy()
+        h_in = h_in if args.dtype == "f64" else h_in.view(np.uint32 if key_bytes == 4 else np.uint64)
         h_buf = np.zeros_like(h_in)  # the caller's output block, already paged in
         res = {}
         for name, chunk in (("staged_overlapped", 1 << 24), ("one_chunk", loc)):

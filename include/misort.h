@@ -261,7 +261,9 @@ int misort_profile_stage(misort_ctx* ctx, int stage, int64_t* count, double* exc
  * (at most 2^20 are kept).  For per-pass roofline figures. */
 int misort_profile_trace(misort_ctx* ctx, int max, int* kinds, double* ms, double* bytes);
 
-/* log2 of the SORT tile (keys) used for a key width of 4 or 8 bytes. */
+/* log2 of the LARGEST SORT tile (keys) for a key width of 4 or 8 bytes: every
+ * plan's tiles divide it.  The tile a given size actually uses is chosen per
+ * size (u32: 2^14 or 2^15); it is the first pass of misort_plan (hi + 1). */
 int misort_tile_log2(int key_bytes);
 
 /* The HBM pass plan of a local sort of n keys (key_bytes 4 or 8), for tools

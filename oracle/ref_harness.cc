@@ -135,7 +135,11 @@ static int keys_mode(int argc, char** argv) {
         for (long long k = 0; k < loc; ++k) {
             uint64_t z = splitmix_at(seed, off + k);
             if (w == 4) { uint32_t v = (uint32_t)(z >> 32); memcpy(&raw[k * 4], &v, 4); }
-            else memcpy(&raw[k * 8], &z, 8);
+            else if (dtype == "f64") {
+                // bench.py's f64 workload: the top 53 bits as a uniform double in [0, 1)
+                const double d = (double)(z >> 11) * 0x1p-53;
+                memcpy(&raw[k * 8], &d, 8);
+            } else memcpy(&raw[k * 8], &z, 8);
         }
     } else if (loc > 0) {
         ssize_t got = pread(fd, raw.data(), (size_t)loc * w, (off_t)(off * (long long)w));

@@ -99,12 +99,6 @@ struct KT<uint64_t> {
     typedef uint64_t vec __attribute__((ext_vector_type(2)));
 };
 
-__device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
-    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-__device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
-    return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
-}
 
 // u64 compare-exchanges on one v_cmp_u64 (cx); register stages batch their
 // compares ahead of the selects (reg_stages_c).
@@ -621,12 +615,20 @@ __device__ __forceinline__ void final_store_plain(const K* s, K* out, int64_t ti
 // phases (wave-local ones without a workgroup barrier).  PERSIST: the grid is
 // smaller than the tile list and every workgroup walks tiles with the next
 // tile's loads in flight; otherwise one tile per workgroup.
+// The first level the u64 SORT tile merges in LDS (0: the whole tile is the
+// network): one condition for the kernel and its launcher, so a probe build
+// with a lower MISORT_SORT_TOP_U64 keeps the persistent grid of the network tile.
+template <typename K, int LT>
+constexpr int sort_tile_mf() {
+    return sizeof(K) == 8 && MISORT_SORT_MERGE_U64 > 0 && MISORT_SORT_TOP_U64 >= LT ? MISORT_SORT_MERGE_U64 : 0;
+}
+
 template <typename K, int LT, bool ORD, bool PERSIST>
 __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_sort_tile(
     const K* in, K* out, int64_t n, int64_t ntiles, void* fence, int flk) {
     typedef TileGeo<K, LT> G;
     // MISORT_SORT_MERGE_U64 = F: levels F..LT as in-LDS merge levels
-    constexpr int MF = sizeof(K) == 8 && MISORT_SORT_TOP_U64 >= LT ? MISORT_SORT_MERGE_U64 : 0;
+    constexpr int MF = sort_tile_mf<K, LT>();
     typedef SortMergeShape<K, LT, MF ? MF : 12> MS;
     // MERGE: 2 keys below the tile (a co-rank probe may read index -1; 16-byte alignment)
     constexpr int WORDS = MF && MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T);
@@ -703,7 +705,7 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
     static int64_t cap = 0;  // resident workgroups
     const int64_t ntiles = (n + G::T - 1) >> LT;
     // the merge-level tile runs one tile per workgroup (see MISORT_SORT_MERGE)
-    const bool persist = !(sizeof(K) == 8 && MISORT_SORT_MERGE_U64 > 0) && plan_knobs().persist_sort((int)sizeof(K));
+    const bool persist = sort_tile_mf<K, LT>() == 0 && plan_knobs().persist_sort((int)sizeof(K));
     if (persist && cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;
         (void)hipGetDevice(&dev);
@@ -949,7 +951,7 @@ void launch_sort(const K* src, K* dst, int64_t n, bool ord_in, hipStream_t s, in
 
 template <typename K>
 hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                           LaunchHook* hook, const StageIO* io) {
+                           LaunchHook* hook, const StageIO* io, bool ord_out) {
     // merge passes ping-pong between out and scratch
     if (scratch == nullptr || scratch == out || scratch == in) return hipErrorInvalidValue;
     const std::vector<Pass>& ps = plan_for<K>(n);
@@ -977,7 +979,15 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
             // by the HookScope marker above; binding there too would record it
             // twice, from a stale start); a marker hook nests k_mergek's record
             LaunchHook* kh = bind || !(hook && hook->binds()) ? hook : nullptr;
-            const hipError_t e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh);
+            hipError_t e;
+            if constexpr (sizeof(K) == 8) {
+                // the last pass stores IEEE double bits itself
+                const bool oo = ord_out && i == np - 1;
+                e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh, oo);
+                if (oo && e == hipSuccess) ord_out = false;
+            } else {
+                e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh);
+            }
             if (e != hipSuccess) return e;
             fence_phase ^= 1;
             src = dst;
@@ -1016,6 +1026,14 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
         }
         src = dst;
     }
+    // a last pass that could not map the keys back (a SORT or 2-way pass:
+    // small sorts, u64 levels past 2^29): one more sweep
+    if constexpr (sizeof(K) == 8) {
+        if (ord_out) {
+            const hipError_t e = ord_to_f64((uint64_t*)out, n, s);
+            if (e != hipSuccess) return e;
+        }
+    }
     return hipGetLastError();
 }
 
@@ -1024,10 +1042,12 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
 // Definition shared by sort_u32.hip / sort_u64.hip (one explicit instantiation each).
 template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                      LaunchHook* hook, const StageIO* io) {
+                      LaunchHook* hook, const StageIO* io, bool ord_out) {
     if (n <= 0) return hipSuccess;
-    if (sizeof(K) == 4 && ord_in) return hipErrorInvalidValue;
-    return local_sort_impl<K>(in, out, n, ord_in, scratch, s, hook, io);
+    if (sizeof(K) == 4 && (ord_in || ord_out)) return hipErrorInvalidValue;
+    // chunked output hands every chunk to after_last, which maps it itself
+    if (ord_out && io && io->after_last) return hipErrorInvalidValue;
+    return local_sort_impl<K>(in, out, n, ord_in, scratch, s, hook, io, ord_out);
 }
 
 // One pass of a plan's shape (probes and tests): the SORT tile pass over n keys

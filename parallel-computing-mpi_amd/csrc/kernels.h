@@ -9,6 +9,15 @@
 
 namespace misort {
 
+// IEEE double bits <-> order-preserving u64 (negative: all bits flipped; else
+// the sign bit set), so every kernel compares unsigned integers.
+__device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
+    return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+}
+
 // Kernel families, used for per-launch profiling (HIP events) and reporting.
 enum Kind : int {
     KIND_TILE_SORT = 0,   // levels 1..LT inside one LDS tile
@@ -77,9 +86,12 @@ struct StageIO {
 // then stays in that ordered form.  scratch (n keys, distinct from in and out,
 // or nullptr) lets the passes ping-pong between two buffers instead of
 // rewriting `out` in place (copy-shaped HBM traffic).
+// ord_out (K = uint64_t): the output is mapped back to IEEE double bits --
+// by the last pass's stores when it is a multi-way pass, else by one more
+// sweep (small sorts).
 template <typename K>
 hipError_t local_sort(const K* in, K* out, int64_t n, bool ord_in, K* scratch, hipStream_t s,
-                      LaunchHook* hook, const StageIO* io = nullptr);
+                      LaunchHook* hook, const StageIO* io = nullptr, bool ord_out = false);
 
 // One HBM pass of a plan's shape over n keys (kind KIND_TILE_SORT, KIND_RUNS
 // or KIND_RUNSK; hi, R as in the plan): probes and tests.
@@ -89,9 +101,10 @@ hipError_t run_pass(const K* in, K* out, int64_t n, int kind, int hi, int R, int
 // Compare-split merge (device half of psort.cc:116-164): out[0..na) = the na
 // smallest (keep_max=0) or largest (keep_max=1) keys of A U B, ascending.
 // scratch must hold ceil(na/2048)+1 int64 co-ranks.
+// ord_out (K = uint64_t): out gets IEEE double bits (the sort's last stage over f64 keys).
 template <typename K>
 hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
-                       int keep_max, int64_t* scratch, hipStream_t s, LaunchHook* hook);
+                       int keep_max, int64_t* scratch, hipStream_t s, LaunchHook* hook, bool ord_out = false);
 
 // Full merge of two ascending runs: out[0..na+nb) (A first on ties; for pure
 // keys the result equals std::sort of the concatenation).  scratch holds
@@ -122,8 +135,10 @@ hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, i
                         bool gather, int lk_next, LaunchHook* hook = nullptr);
 // u64 keys: the same with 128-bit fences (key << 64 | run/position tag);
 // 13 <= lw, lw + lk <= 29.
+// ord_out: the pass is the sort's last (lk_next = 0) and writes IEEE double
+// bits (f64_of_ord in its stores: no separate back-conversion sweep).
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next, LaunchHook* hook = nullptr);
+                        bool gather, int lk_next, LaunchHook* hook = nullptr, bool ord_out = false);
 int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
 // Fence stride of the multi-way passes (log2 keys).
 #ifndef MISORT_MK_FG_LOG2
@@ -176,6 +191,7 @@ hipError_t exchange_count(const K* sa, int64_t na, const K* sb, int64_t nb, int 
 // IEEE double bits <-> order-preserving u64, in place.
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s);
 hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s);
+hipError_t ord_to_f64_copy(const uint64_t* a, uint64_t* b, int64_t n, hipStream_t s);  // b = f64 bits of a
 
 // Counter-based SplitMix64 keys for global indices [g0, g0+n) (bench/test input).
 hipError_t fill_splitmix_u32(uint32_t* out, int64_t n, uint64_t seed, int64_t g0, hipStream_t s);

@@ -19,6 +19,12 @@ PlanKnobs::PlanKnobs() {
     env("MISORT_MULTIWAY_U64", multiway_u64);
     env("MISORT_SORT_TILE_U32", sort_tile_u32);
     if (grid_mult < 1) grid_mult = 1;
+    if (sort_tile_u32 != 0 && sort_tile_u32 != SORT_LT_MERGE && sort_tile_u32 != SORT_LT_U32) {
+        // a pin the plan cannot honour would silently measure the per-size rule
+        fprintf(stderr, "misort: MISORT_SORT_TILE_U32=%d ignored (0, %d or %d); the tile is chosen per size\n",
+                sort_tile_u32, SORT_LT_MERGE, SORT_LT_U32);
+        sort_tile_u32 = 0;
+    }
 }
 
 const PlanKnobs& plan_knobs() {
@@ -72,7 +78,9 @@ __global__ void k_merge_partition(const K* __restrict__ A, int64_t na, const K* 
 
 // Output keys [d0 + t*TILE, ...) of merge(A, B): each workgroup stages its A
 // and B ranges in LDS, each lane merges MS_ITEMS consecutive outputs.
-template <typename K>
+// ORD (u64 only): the stage is the sort's last over f64 keys; the outputs
+// are stored as IEEE double bits (no separate back-conversion sweep).
+template <typename K, bool ORD = false>
 __global__ __launch_bounds__(MS_NT) void k_merge_tiles(const K* __restrict__ A, int64_t na,
                                                        const K* __restrict__ B, int64_t nb,
                                                        int64_t d0, int64_t nout,
@@ -123,7 +131,10 @@ __global__ __launch_bounds__(MS_NT) void k_merge_tiles(const K* __restrict__ A, 
     for (int k = 0; k < MS_ITEMS; ++k)
         if (dk + k < len) s[dk + k] = r[k];
     __syncthreads();
-    for (int k = threadIdx.x; k < len; k += MS_NT) out[ds + k] = s[k];
+    for (int k = threadIdx.x; k < len; k += MS_NT) {
+        if constexpr (ORD) out[ds + k] = (K)f64_of_ord((uint64_t)s[k]);
+        else out[ds + k] = s[k];
+    }
 }
 
 // ---------------------------------------------------------------- helpers
@@ -230,10 +241,11 @@ __global__ void k_bounds(const K* __restrict__ a, int64_t n, const K* __restrict
     ub[v] = lo;
 }
 
-__global__ void k_f64_ord(uint64_t* a, int64_t n, int to_ord) {
+// b[i] = map(a[i]) (a == b: in place)
+__global__ void k_f64_ord(const uint64_t* a, uint64_t* b, int64_t n, int to_ord) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        a[i] = to_ord ? ord_of_f64(a[i]) : f64_of_ord(a[i]);
+        b[i] = to_ord ? ord_of_f64(a[i]) : f64_of_ord(a[i]);
 }
 
 __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, int64_t g) {
@@ -262,14 +274,16 @@ int stream_grid(int64_t n, int threads) {
 
 template <typename K>
 hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out, int keep_max,
-                       int64_t* scratch, hipStream_t s, LaunchHook* hook) {
+                       int64_t* scratch, hipStream_t s, LaunchHook* hook, bool ord_out) {
     if (na <= 0) return hipSuccess;
+    if (ord_out && sizeof(K) != 8) return hipErrorInvalidValue;
     const int64_t d0 = keep_max ? nb : 0;
     const int64_t ntiles = (na + MS_TILE - 1) / MS_TILE;
     HookScope hs(hook, KIND_MERGE_SPLIT, (double)(2 * na + (nb < na ? nb : na)) * sizeof(K), s);
     k_merge_partition<K><<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, s>>>(a, na, b, nb, d0, na,
                                                                               ntiles, scratch);
-    k_merge_tiles<K><<<(unsigned)ntiles, MS_NT, 0, s>>>(a, na, b, nb, d0, na, scratch, out);
+    if (ord_out) k_merge_tiles<K, true><<<(unsigned)ntiles, MS_NT, 0, s>>>(a, na, b, nb, d0, na, scratch, out);
+    else k_merge_tiles<K><<<(unsigned)ntiles, MS_NT, 0, s>>>(a, na, b, nb, d0, na, scratch, out);
     return hipGetLastError();
 }
 
@@ -330,13 +344,15 @@ template hipError_t exchange_count<uint64_t>(const uint64_t*, int64_t, const uin
 
 hipError_t f64_to_ord(uint64_t* a, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    k_f64_ord<<<stream_grid(n, 256), 256, 0, s>>>(a, n, 1);
+    k_f64_ord<<<stream_grid(n, 256), 256, 0, s>>>(a, a, n, 1);
     return hipGetLastError();
 }
 
-hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s) {
+hipError_t ord_to_f64(uint64_t* a, int64_t n, hipStream_t s) { return ord_to_f64_copy(a, a, n, s); }
+
+hipError_t ord_to_f64_copy(const uint64_t* a, uint64_t* b, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    k_f64_ord<<<stream_grid(n, 256), 256, 0, s>>>(a, n, 0);
+    k_f64_ord<<<stream_grid(n, 256), 256, 0, s>>>(a, b, n, 0);
     return hipGetLastError();
 }
 
@@ -353,9 +369,9 @@ hipError_t fill_splitmix_u64(uint64_t* out, int64_t n, uint64_t seed, int64_t g0
 }
 
 template hipError_t merge_split<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int64_t,
-                                          uint32_t*, int, int64_t*, hipStream_t, LaunchHook*);
+                                          uint32_t*, int, int64_t*, hipStream_t, LaunchHook*, bool);
 template hipError_t merge_split<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t,
-                                          uint64_t*, int, int64_t*, hipStream_t, LaunchHook*);
+                                          uint64_t*, int, int64_t*, hipStream_t, LaunchHook*, bool);
 template hipError_t merge_full<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int64_t, uint32_t*,
                                          int64_t*, hipStream_t, LaunchHook*);
 template hipError_t merge_full<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t, uint64_t*,

@@ -903,7 +903,26 @@ __device__ __forceinline__ int row_part(int tid) {
 // The chunk's in-LDS work after its keys and sentinels are in LDS: the merge
 // levels, the outputs back to LDS (shifted so every 16-byte global vector is
 // one aligned LDS vector), out to HBM, and the next pass's fences.
-template <typename KEY, int LK, bool FENCES, int MODE>
+// The key as stored: ORD (u64, the sort's last pass over f64 keys) maps the
+// ordered form back to IEEE double bits.
+template <bool ORD, typename KEY>
+__device__ __forceinline__ KEY out_key(KEY k) {
+    if constexpr (ORD) return (KEY)f64_of_ord((uint64_t)k);
+    else return k;
+}
+template <bool ORD, typename V>
+__device__ __forceinline__ V out_vec(V v) {
+    if constexpr (ORD) {
+        V o;
+#pragma unroll
+        for (int j = 0; j < (int)(sizeof(V) / sizeof(uint64_t)); ++j) o[j] = f64_of_ord(v[j]);
+        return o;
+    } else {
+        return v;
+    }
+}
+
+template <typename KEY, int LK, bool FENCES, int MODE, bool ORD = false>
 __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY* __restrict__ dst,
                                              typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid) {
     typedef Shape<KEY, LK> S;
@@ -947,11 +966,12 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
     for (int v = tid; v < nv; v += NT) {
         const int e = VK * v;
         if (e >= sh && e + VK <= sh + len) {
-            __builtin_nontemporal_store(*reinterpret_cast<const kvec<KEY>*>(s + e), reinterpret_cast<kvec<KEY>*>(o + e));
+            __builtin_nontemporal_store(out_vec<ORD>(*reinterpret_cast<const kvec<KEY>*>(s + e)),
+                                        reinterpret_cast<kvec<KEY>*>(o + e));
         } else {
 #pragma unroll
             for (int j = 0; j < VK; ++j)
-                if (e + j >= sh && e + j < sh + len) o[e + j] = s[e + j];
+                if (e + j >= sh && e + j < sh + len) o[e + j] = out_key<ORD>(s[e + j]);
         }
     }
     if constexpr (FENCES) {
@@ -988,7 +1008,7 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
 // attribution: 3 - 1 = the searches, 0 - 3 = the chains).
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
-template <typename KEY, int LK, bool FENCES, int MODE = 0>
+template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
 __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256) void k_mergek(
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
@@ -1043,7 +1063,7 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
         mergek_sentinels<KEY, LK>(s, d, tid);
     }
     __syncthreads();
-    mergek_chunk<KEY, LK, FENCES, MODE>(s, d, dst, fout, lwn, lkn, tid);
+    mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid);
 }
 
 // Fence buffers, bounds and descriptors: one grow-only set per (device, stream).
@@ -1097,7 +1117,7 @@ int64_t chunks_of(const Geo& geo) {
 
 template <typename KEY, int LK>
 hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
-                      int lk_next, LaunchHook* hook) {
+                      int lk_next, LaunchHook* hook, bool ord_out) {
     typedef Shape<KEY, LK> S;
     typedef typename KTr<KEY>::F FT;
     const Geo geo = make_geo<KEY>(n, lw, LK);
@@ -1221,6 +1241,9 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     if (lk_next > 0) {
         launch_timed(k_mergek<KEY, LK, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next);
+    } else if (sizeof(KEY) == 8 && ord_out) {
+        launch_timed(k_mergek<KEY, LK, false, 0, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
+                     (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
     } else {
         launch_timed(k_mergek<KEY, LK, false>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
@@ -1246,17 +1269,17 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
 
 template <typename KEY>
 hipError_t merge_levelk_t(const KEY* src, KEY* dst, int64_t n, int lw, int lk, hipStream_t s, int phase, bool gather,
-                          int lk_next, LaunchHook* hook) {
+                          int lk_next, LaunchHook* hook, bool ord_out = false) {
     if (n <= 0) return hipSuccess;
     // load rows address a group with 32-bit byte offsets (KW * sizeof(KEY) <=
     // 2^32); runs at least a SORT tile long
     if (lk < 1 || lk > 4 || lw < KTr<KEY>::LW_MIN || lw + lk > KTr<KEY>::LWK_MAX || src == dst || lk_next < 0 ||
-        lk_next > 4)
+        lk_next > 4 || (ord_out && (sizeof(KEY) != 8 || lk_next > 0)))
         return hipErrorInvalidValue;
-    if (lk == 1) return merge_pass<KEY, 1>(src, dst, n, lw, s, phase, gather, lk_next, hook);
-    if (lk == 2) return merge_pass<KEY, 2>(src, dst, n, lw, s, phase, gather, lk_next, hook);
-    if (lk == 3) return merge_pass<KEY, 3>(src, dst, n, lw, s, phase, gather, lk_next, hook);
-    return merge_pass<KEY, 4>(src, dst, n, lw, s, phase, gather, lk_next, hook);
+    if (lk == 1) return merge_pass<KEY, 1>(src, dst, n, lw, s, phase, gather, lk_next, hook, ord_out);
+    if (lk == 2) return merge_pass<KEY, 2>(src, dst, n, lw, s, phase, gather, lk_next, hook, ord_out);
+    if (lk == 3) return merge_pass<KEY, 3>(src, dst, n, lw, s, phase, gather, lk_next, hook, ord_out);
+    return merge_pass<KEY, 4>(src, dst, n, lw, s, phase, gather, lk_next, hook, ord_out);
 }
 
 }  // namespace
@@ -1274,8 +1297,8 @@ hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, i
     return merge_levelk_t<uint32_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook);
 }
 hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
-                        bool gather, int lk_next, LaunchHook* hook) {
-    return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook);
+                        bool gather, int lk_next, LaunchHook* hook, bool ord_out) {
+    return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook, ord_out);
 }
 void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
     // the sizes merge_pass computes, so the buffer never moves between the two

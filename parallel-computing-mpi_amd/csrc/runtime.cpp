@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <mutex>
+#include <set>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -243,6 +244,12 @@ struct Profiler final : misort::LaunchHook {
     }
 };
 
+// The context's small device words (sizes, counts, check_sort's words) are
+// one buffer of this size from its first use: growing it would hipFree the
+// old one, which waits for the whole device -- with no deadline behind a
+// transfer from a dead peer.
+constexpr size_t kSmallBytes = 256;
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -301,6 +308,9 @@ struct Transport {
     // Wait for stream s, whose queue may hold transfers from other ranks,
     // within peer_timeout_s().
     virtual int wait(hipStream_t s) = 0;
+    // Stream s may hold a transfer from another rank (a copy from pageable
+    // host memory enqueued behind it would block the host with no deadline).
+    virtual bool busy(hipStream_t) const { return false; }
     // A rank failed inside a collective call: make the failure collective
     // (the reference MPI_Abort's, psort.cc:170), so the other ranks error out
     // instead of waiting for this one.  The transport is unusable afterwards.
@@ -394,12 +404,18 @@ struct RcclTransport final : Transport {
     // remote failure or the deadline aborts the communicator and returns
     // MISORT_E_RCCL.  Spins briefly (stage waits are usually short), then
     // sleeps between polls.
-    uint64_t drained_calls = 0;  // `calls` at the last wait that drained the stream
+    // Streams with a transport call queued since they last drained under
+    // wait(): a caller may queue a sort on its own stream and drain another
+    // one first, so the record is per stream (one per transport would let the
+    // other stream's drain clear this one's, and a dead peer would then hang
+    // the plain synchronisation below).
+    std::set<hipStream_t> pending;
+    bool busy(hipStream_t s) const override { return pending.count(s) != 0; }
     int wait(hipStream_t s) override {
         int rc = usable();
         if (rc) return rc;
-        if (calls == drained_calls) {
-            // no transport call since the stream last drained: only local work
+        if (!pending.count(s)) {
+            // no transport call on s since it last drained: only local work
             // is queued (it may legitimately run longer than the peer deadline,
             // e.g. under a counter-collecting profiler), so no deadline and no abort
             HIPCHK(hipStreamSynchronize(s));
@@ -411,7 +427,7 @@ struct RcclTransport final : Transport {
         for (int it = 0;; ++it) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {
-                drained_calls = calls;
+                pending.erase(s);
                 return MISORT_OK;
             }
             if (q != hipErrorNotReady) {
@@ -436,10 +452,11 @@ struct RcclTransport final : Transport {
     // ncclGroupStart ... ncclGroupEnd that always closes the group, also when
     // a call inside it fails, under the call watchdog.
     template <typename F>
-    int grouped(const char* what, F&& body) {
+    int grouped(const char* what, hipStream_t s, F&& body) {
         ++calls;
         int rc = usable();
         if (rc) return rc;
+        pending.insert(s);
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess) return rccl_fail("ncclGroupStart", r);
         ncclResult_t inner = body();
@@ -467,7 +484,7 @@ struct RcclTransport final : Transport {
         if (rc) return rc;
         HIPCHK(hipMemsetAsync(tmp.p, 0, tmp.bytes, s));
         char* b = (char*)tmp.p;
-        rc = grouped("connect: ncclSend/ncclRecv with every peer", [&] {
+        rc = grouped("connect: ncclSend/ncclRecv with every peer", s, [&] {
             ncclResult_t r = ncclSuccess;
             for (int k = 1; k < nranks && r == ncclSuccess; ++k) {
                 const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
@@ -487,7 +504,7 @@ struct RcclTransport final : Transport {
     }
     int allgather_dev(const int64_t* d_src, int count, std::vector<int64_t>& all, hipStream_t s) {
         int64_t* d = (int64_t*)buf.p;
-        int rc = grouped("ncclAllGather", [&] { return ncclAllGather(d_src, d, count, ncclInt64, comm, s); });
+        int rc = grouped("ncclAllGather", s, [&] { return ncclAllGather(d_src, d, count, ncclInt64, comm, s); });
         if (rc) return rc;
         // drain the stream under the deadline first: a device-to-host copy
         // into pageable memory would block on it without one
@@ -500,6 +517,9 @@ struct RcclTransport final : Transport {
     int allgather_i64(const int64_t* mine, int count, std::vector<int64_t>& all, hipStream_t s) override {
         int rc = usable();
         if (rc || (rc = buf.ensure(sizeof(int64_t) * (size_t)count * (nranks + 1)))) return rc;
+        // the copy below is from pageable memory: behind a transfer from a
+        // dead peer it would block with no deadline, so drain under one first
+        if (busy(s) && (rc = wait(s))) return rc;
         int64_t* d = (int64_t*)buf.p;
         HIPCHK(hipMemcpyAsync(d + (size_t)count * nranks, mine, sizeof(int64_t) * count,
                               hipMemcpyHostToDevice, s));
@@ -511,7 +531,7 @@ struct RcclTransport final : Transport {
         return allgather_dev(d_mine, count, all, s);
     }
     int sendrecv(const void* send, size_t sb, void* recv, size_t rb, int peer, hipStream_t s) override {
-        return grouped("ncclSend/ncclRecv", [&] {
+        return grouped("ncclSend/ncclRecv", s, [&] {
             ncclResult_t r = ncclSuccess;
             if (sb) r = ncclSend(send, sb, ncclUint8, peer, comm, s);
             if (r == ncclSuccess && rb) r = ncclRecv(recv, rb, ncclUint8, peer, comm, s);
@@ -519,7 +539,7 @@ struct RcclTransport final : Transport {
         });
     }
     int group_p2p(const std::vector<Op>& ops, hipStream_t s) override {
-        return grouped("grouped ncclSend/ncclRecv", [&] {
+        return grouped("grouped ncclSend/ncclRecv", s, [&] {
             ncclResult_t r = ncclSuccess;
             for (const Op& o : ops) {
                 if (!o.bytes || r != ncclSuccess) continue;
@@ -536,7 +556,7 @@ struct RcclTransport final : Transport {
         if (scnt[rank])
             HIPCHK(hipMemcpyAsync((char*)recv + roff[rank], (const char*)send + soff[rank], (size_t)scnt[rank],
                                   hipMemcpyDeviceToDevice, s));
-        return grouped("all-to-all-v ncclSend/ncclRecv", [&] {
+        return grouped("all-to-all-v ncclSend/ncclRecv", s, [&] {
             ncclResult_t r = ncclSuccess;
             for (int k = 1; k < nranks && r == ncclSuccess; ++k) {
                 const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
@@ -790,6 +810,18 @@ int sync(misort_ctx* c, hipStream_t s) {
     return MISORT_OK;
 }
 
+// A small host -> device copy from pageable memory on stream s: such a copy
+// blocks the host until the stream reaches it, so a stream that may hold a
+// transfer from another rank is drained under the peer deadline first.
+int h2d(misort_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (c->tr && c->tr->busy(s)) {
+        const int rc = c->tr->wait(s);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    return MISORT_OK;
+}
+
 // Small device -> host copies after work that may include transfers from
 // other ranks: the stream is drained first by the bounded wait (a copy into
 // pageable memory would block on an undrained stream with no deadline).
@@ -829,7 +861,7 @@ int collective_result(misort_ctx* c, uint64_t calls0, int rc) {
 }
 
 int do_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, bool ord_in,
-                  hipStream_t s, const misort::StageIO* io = nullptr) {
+                  hipStream_t s, const misort::StageIO* io = nullptr, bool ord_out = false) {
     // scratch for the ping-pong passes (grown on demand, kept for the context)
     int rc = c->pong.ensure(std::max<size_t>(16, (size_t)n * key_bytes(dtype)));
     if (rc) return rc;
@@ -839,13 +871,13 @@ int do_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t n
                                          hook(c), io);
     else
         e = misort::local_sort<uint64_t>((const uint64_t*)in, (uint64_t*)out, n, ord_in, (uint64_t*)c->pong.p, s,
-                                         hook(c), io);
+                                         hook(c), io, ord_out);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "local_sort: %s", hipGetErrorString(e));
     return MISORT_OK;
 }
 
 int do_merge_split(misort_ctx* c, int dtype, const void* a, int64_t na, const void* b, int64_t nb,
-                   void* out, int keep_max, hipStream_t s) {
+                   void* out, int keep_max, hipStream_t s, bool ord_out = false) {
     const int64_t ntiles = (na + 2047) / 2048 + 2;
     int rc = c->scratch.ensure((size_t)ntiles * sizeof(int64_t));
     if (rc) return rc;
@@ -855,7 +887,7 @@ int do_merge_split(misort_ctx* c, int dtype, const void* a, int64_t na, const vo
                                           (uint32_t*)out, keep_max, (int64_t*)c->scratch.p, s, hook(c));
     else
         e = misort::merge_split<uint64_t>((const uint64_t*)a, na, (const uint64_t*)b, nb,
-                                          (uint64_t*)out, keep_max, (int64_t*)c->scratch.p, s, hook(c));
+                                          (uint64_t*)out, keep_max, (int64_t*)c->scratch.p, s, hook(c), ord_out);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "merge_split: %s", hipGetErrorString(e));
     return MISORT_OK;
 }
@@ -973,11 +1005,11 @@ int relay_sizes(misort_ctx* c, const int64_t* d_pair, std::vector<int64_t>& pair
 // A relayed raw (or empty) message of `bytes` (a multiple of 4): the size
 // round is relay_sizes with coded = raw.
 int relay_raw(misort_ctx* c, int bit, const void* sbuf, size_t bytes, void* rbuf, size_t rbytes, hipStream_t s) {
-    int rc = c->small.ensure(64);
+    int rc = c->small.ensure(kSmallBytes);
     if (rc) return rc;
     int64_t* d_sz = (int64_t*)c->small.p + 2;
     const int64_t w2[2] = {(int64_t)(bytes / 4), (int64_t)(bytes / 4)};
-    HIPCHK(hipMemcpyAsync(d_sz, w2, 16, hipMemcpyHostToDevice, s));
+    if ((rc = h2d(c, d_sz, w2, 16, s))) return rc;
     std::vector<int64_t> pairs, units;
     if ((rc = relay_sizes(c, d_sz, pairs, units, s))) return rc;
     return relay_exchange(c, 4, bit, sbuf, bytes, rbuf, rbytes, s, nullptr, &units);
@@ -1136,7 +1168,9 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
             };
         }
     }
-    if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s, io ? &lio : nullptr))) return rc;
+    // no compare-split after the local sort: its last pass writes f64 bits
+    bool ord_done = f64 && nst == 0 && !chunk_out;
+    if ((rc = do_local_sort(c, dtype, in, cur, loc, f64, s, io ? &lio : nullptr, ord_done))) return rc;
     if (chunk_out && chunked) return MISORT_OK;  // after_last owned the f64 back-conversion
     if (chunk_out) {
         // a last pass that is not chunked (a multi-way pass): the caller copies
@@ -1181,7 +1215,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         const bool relayed = c->relay && p > 2;
         const void* rkeys = c->recv.p;
         const int64_t moved0 = c->xchg_bytes;
-        if ((rc = c->small.ensure(64))) return rc;
+        if ((rc = c->small.ensure(kSmallBytes))) return rc;
         int64_t* d_run = (int64_t*)c->small.p + 4;  // {send offset, k} on the device
         // the codec's offsets and word totals are 32-bit: messages that could
         // reach 2^32 words go raw (both sides decide from the same bound)
@@ -1219,7 +1253,10 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                 continue;
             }
             xg_close((double)(c->xchg_bytes - moved0));
-            if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, k, other, keep[st], s))) return rc;
+            // the last stage, writing `out`: f64 bits straight from the merge
+            const bool oo = f64 && st == nst - 1 && other == out;
+            if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, k, other, keep[st], s, oo))) return rc;
+            ord_done = ord_done || oo;
             std::swap(cur, other);
             continue;
         }
@@ -1268,11 +1305,17 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         c->xchg_bytes += (int64_t)(sbytes + rbytes);
         c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
         xg_close((double)(c->xchg_bytes - moved0));
-        if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
+        const bool oo = f64 && st == nst - 1 && other == out;
+        if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s, oo))) return rc;
+        ord_done = ord_done || oo;
         std::swap(cur, other);
     }
-    if (cur != out && loc > 0) HIPCHK(hipMemcpyAsync(out, cur, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
-    if (f64) HIPCHK(misort::ord_to_f64((uint64_t*)out, loc, s));
+    if (f64 && !ord_done && loc > 0) {
+        // one sweep: copy (skipped stages left the keys in `work`) and map back together
+        HIPCHK(misort::ord_to_f64_copy((const uint64_t*)cur, (uint64_t*)out, loc, s));
+    } else if (cur != out && loc > 0) {
+        HIPCHK(hipMemcpyAsync(out, cur, (size_t)loc * w, hipMemcpyDeviceToDevice, s));
+    }
     return MISORT_OK;
 }
 
@@ -1327,7 +1370,7 @@ int parallel_quick(misort_ctx* c, int dtype, const void* in, int64_t loc, void* 
         const int64_t keep_off = low ? 0 : pi, keep_n = low ? pi : rs - pi;
         const int64_t send_off = low ? pi : 0, send_n = low ? rs - pi : pi;
         // MPI_Send/MPI_Recv + MPI_Get_count (psort.cc:438-471): counts first, then keys
-        HIPCHK(hipMemcpyAsync(dcnt, &send_n, 8, hipMemcpyHostToDevice, s));
+        if ((rc = h2d(c, dcnt, &send_n, 8, s))) return rc;
         if ((rc = c->tr->sendrecv(dcnt, 8, dcnt + 1, 8, partner, s))) return rc;
         int64_t recv_n = 0;
         if ((rc = fetch(c, s, {{&recv_n, dcnt + 1, 8}}))) return rc;
@@ -1439,7 +1482,7 @@ int parallel_sample(misort_ctx* c, int dtype, const void* in, void* out, int64_t
         if ((rc = c->qcnt.ensure((size_t)ns * 16 + 64))) return rc;
         int64_t* dlb = (int64_t*)c->qcnt.p;
         int64_t* dub = dlb + ns;
-        HIPCHK(hipMemcpyAsync(c->samp_peer.p, vals.data(), vals.size(), hipMemcpyHostToDevice, s));
+        if ((rc = h2d(c, c->samp_peer.p, vals.data(), vals.size(), s))) return rc;
         hipError_t e = w == 4 ? misort::bounds<uint32_t>((const uint32_t*)c->qa.p, loc, (const uint32_t*)c->samp_peer.p,
                                                          ns, dlb, dub, s)
                               : misort::bounds<uint64_t>((const uint64_t*)c->qa.p, loc, (const uint64_t*)c->samp_peer.p,
@@ -1697,7 +1740,7 @@ int misort_codec_probe(misort_ctx* c, int dtype, const void* keys, int64_t n, in
     if ((rc = c->enc_send.ensure((size_t)misort::codec_max_words(n, (int)w) * 4))) return rc;
     const size_t scr = misort::codec_scratch_bytes(n) + 64;
     if ((rc = c->codec_scr.ensure(scr))) return rc;
-    if ((rc = c->small.ensure(64))) return rc;
+    if ((rc = c->small.ensure(kSmallBytes))) return rc;
     if ((rc = c->recv.ensure((size_t)n * w))) return rc;
     void* out = decoded ? decoded : c->recv.p;
     hipStream_t s = c->stream;
@@ -1794,10 +1837,8 @@ int misort_local_sort(misort_ctx* c, int dtype, const void* in, void* out, int64
     if (!c || !valid_dtype(dtype) || n < 0 || (n > 0 && (!in || !out)))
         return fail(MISORT_E_INVALID, "bad local_sort arguments");
     hipStream_t s = pick(c, stream);
-    int rc = do_local_sort(c, dtype, in, out, n, dtype == MISORT_F64, s);
-    if (rc) return rc;
-    if (dtype == MISORT_F64) HIPCHK(misort::ord_to_f64((uint64_t*)out, n, s));
-    return MISORT_OK;
+    // f64: mapped to ordered u64 by the first pass, back by the last
+    return do_local_sort(c, dtype, in, out, n, dtype == MISORT_F64, s, nullptr, dtype == MISORT_F64);
 }
 
 int misort_pass_probe(misort_ctx* c, int dtype, const void* in, void* out, int64_t n, int kind, int hi,
@@ -1890,7 +1931,7 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     hipStream_t s = pick(c, stream);
     const int p = c->nranks;
     // Per rank: {local descents, n, first key bits, last key bits}.
-    int rc = c->small.ensure(sizeof(uint64_t) * 4 + 64);
+    int rc = c->small.ensure(kSmallBytes);
     if (rc) return rc;
     uint64_t* mine = (uint64_t*)c->small.p;
     HIPCHK(hipMemsetAsync(mine, 0, sizeof(uint64_t) * 4, s));
@@ -1899,8 +1940,8 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     else if (dtype == MISORT_U64) e = misort::count_descents<uint64_t>((const uint64_t*)keys, n, (unsigned long long*)mine, s);
     else e = misort::count_descents<double>((const double*)keys, n, (unsigned long long*)mine, s);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "count_descents: %s", hipGetErrorString(e));
-    const uint64_t nn = (uint64_t)n;
-    HIPCHK(hipMemcpyAsync(mine + 1, &nn, 8, hipMemcpyHostToDevice, s));
+    // (n itself is set on the host after the fetch: a copy from pageable
+    // memory behind a pending transfer would block with no deadline)
     const size_t w = key_bytes(dtype);
     if (n > 0) {
         HIPCHK(hipMemcpyAsync(mine + 2, keys, w, hipMemcpyDeviceToDevice, s));
@@ -1910,6 +1951,7 @@ int misort_check_sort(misort_ctx* c, int dtype, const void* keys, int64_t n, int
     // with the rest, so every rank reports it together)
     int64_t four[5];
     if ((rc = fetch(c, s, {{four, mine, 4 * sizeof(int64_t)}}))) return rc;
+    four[1] = n;
     const int perr = planning_check(s);
     if (perr == MISORT_E_HIP) {
         // this rank cannot take part in the gather: abort the communicator so

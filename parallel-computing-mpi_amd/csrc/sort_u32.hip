@@ -4,6 +4,6 @@
 
 namespace misort {
 template hipError_t local_sort<uint32_t>(const uint32_t*, uint32_t*, int64_t, bool, uint32_t*, hipStream_t,
-                                        LaunchHook*, const StageIO*);
+                                        LaunchHook*, const StageIO*, bool);
 template hipError_t run_pass<uint32_t>(const uint32_t*, uint32_t*, int64_t, int, int, int, int, hipStream_t);
 }  // namespace misort

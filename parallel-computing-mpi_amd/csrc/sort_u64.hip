@@ -4,6 +4,6 @@
 
 namespace misort {
 template hipError_t local_sort<uint64_t>(const uint64_t*, uint64_t*, int64_t, bool, uint64_t*, hipStream_t,
-                                        LaunchHook*, const StageIO*);
+                                        LaunchHook*, const StageIO*, bool);
 template hipError_t run_pass<uint64_t>(const uint64_t*, uint64_t*, int64_t, int, int, int, int, hipStream_t);
 }  // namespace misort

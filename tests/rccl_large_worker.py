@@ -14,6 +14,12 @@ only the wire is not xGMI).
     rccl_large_worker.py stall|dead      rank 1 stops taking part (sleeps / exits)
                                          after the communicator is up; rank 0 must
                                          get MISORT_E_RCCL within MISORT_TIMEOUT_S
+    rccl_large_worker.py dead_user_stream both ranks queue a sort on the caller's
+                                         stream; rank 1 exits before its last
+                                         transfer ran; rank 0 drains the context's
+                                         own (idle) stream, then check_sort on the
+                                         caller's stream must still get
+                                         MISORT_E_RCCL within MISORT_TIMEOUT_S
 
 Results are checked against tests/golden/large.json (the oracle's outputs,
 pinned by runs of the compiled reference): each rank writes its block to a
@@ -102,6 +108,36 @@ def main():
             code2 = e.code
         print(json.dumps({"world": world, "mode": mode, "code": code, "msg": msg, "elapsed_s": el,
                           "second_code": code2, "second_s": time.perf_counter() - t1}), flush=True)
+        os._exit(0)
+
+    if mode == "dead_user_stream":
+        import faulthandler
+        faulthandler.dump_traceback_later(90, exit=True)
+        # a whole-block 2^25-key exchange: rank 1's send cannot have finished
+        # when it leaves right after queuing it
+        ctx.set_compress(False)
+        ctx.set_full_exchange(True)
+        n = 1 << 26
+        buf = torch.empty(n // world, dtype=u32_t, device="cuda")
+        ctx.fill_splitmix(buf, 0x5EED0003, rank * (n // world))
+        user = torch.cuda.Stream()
+        user.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        code, msg = 0, ""
+        try:
+            ctx.parallel_bitonic_sort(buf, buf.numel(), buf.numel(), stream=user.cuda_stream)
+            if rank == 1:
+                os._exit(0)  # the last transfer is queued, not done
+            ctx.synchronize()  # the context's own stream: idle, drains at once
+            ctx.check_sort(buf, buf.numel(), stream=user.cuda_stream)
+        except misort.MisortError as e:
+            code, msg = e.code, str(e)
+        el = time.perf_counter() - t0
+        log(f"check_sort on the caller's stream returned {code} after {el:.1f} s: {msg}")
+        print(json.dumps({"world": world, "mode": mode, "code": code, "msg": msg, "elapsed_s": el,
+                          "second_code": code, "second_s": 0.0}), flush=True)
         os._exit(0)
 
     def sort_and_check(name, n, kdt, fill, want_sha, want_err, want_sizes=None):

@@ -15,7 +15,9 @@ tests/rccl_large_worker.py).
 * failure detection: a peer that stalls or dies after the communicator is up
   makes rank 0 fail with MISORT_E_RCCL within MISORT_TIMEOUT_S instead of
   hanging (the reference's alarm(540) watchdog + abort, psort.cc:17,56-65,170),
-  and later calls fail at once.
+  and later calls fail at once; also when the sort was queued on the caller's
+  stream and another stream drained before check_sort (the deadline follows
+  the stream that holds the transfers).
 """
 import json
 import os
@@ -98,7 +100,7 @@ def test_rccl_baseline_size(p, args):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("mode", ["stall", "dead"])
+@pytest.mark.parametrize("mode", ["stall", "dead", "dead_user_stream"])
 def test_rccl_failed_peer_errors_instead_of_hanging(mode):
     limit = 15
     rc, res = launch(2, [mode], timeout=120, extra_env={"MISORT_TIMEOUT_S": str(limit), "MISORT_TRACE": "1",

@@ -104,8 +104,10 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
 out = {"source": os.path.basename(os.path.normpath(root)),
        "workload": os.environ.get("WORKLOAD"),
        "calibration": os.path.relpath(CAL_PATH, HERE) if CAL is not None else "none (FETCH_SIZE x 2)",
-       "note": "bytes per launch = FETCH_SIZE*1024*read_scale(kernel) + WRITE_SIZE*1024*write_scale "
-               "(per-kernel calibrated gfx950 counter correction)"}
+       "note": "bytes per launch = FETCH_SIZE*1024*read_scale(kernel) + WRITE_SIZE*1024*write_scale; "
+               "read scales are calibrated per kernel access shape; the write scale is the 16-B "
+               "streaming store's for every kernel (ASSUMED for the 8-B / 16-B fence, descriptor and "
+               "bounds writers, whose store shapes are not calibrated)"}
 for fam, cs in acc.items():
     f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) if cs.get("FETCH_SIZE") else None
     w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) if cs.get("WRITE_SIZE") else None
