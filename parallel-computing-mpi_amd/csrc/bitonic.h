@@ -514,6 +514,12 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_STOP
 #define MISORT_SORT_STOP 0
 #endif
+#ifndef MISORT_SORT_ZW
+#define MISORT_SORT_ZW 1
+#endif
+#ifndef MISORT_SORT_PT
+#define MISORT_SORT_PT 0
+#endif
 template <typename KEY, int LT, int F>
 struct SortMergeShape {
     static_assert(F >= 7 && F <= 12 && F <= LT, "merge levels from runs of 64 .. 2^11 keys");
@@ -537,6 +543,14 @@ struct SortMergeShape {
     static constexpr int GS = G;
     static constexpr int WORDS = NT * IT + G + 8;  // the level layouts (>= K runs of RUN + GS)
     static_assert(K * (RUN + GS) <= WORDS && (1 << LT) + (K / 2) * (G + QA) <= NT * IT, "SORT merge layout");
+    // zero words below the A sequences and the levels' pair table, as in the
+    // multi-way passes (lds_merge.h; MISORT_SORT_ZW, MISORT_SORT_PT): the
+    // table sits past the level layouts, 16-byte aligned
+    static constexpr bool ZW = MISORT_SORT_ZW && CH == 1;
+    static constexpr bool PT = MISORT_SORT_PT && K > 2;
+    static constexpr int PT_AT = (WORDS + 3) & ~3;
+    static constexpr int PT_WORDS = PT ? (K / 2) * (int)(sizeof(PairRec) / sizeof(KEY)) : 0;
+    static constexpr int ALL_WORDS = PT ? PT_AT + PT_WORDS : WORDS;
 };
 
 // Levels F..LT of a tile whose runs of 2^(F-1) keys are sorted in the padded
@@ -559,18 +573,22 @@ __device__ __forceinline__ void tile_merge_top(KEY* s, int t) {
     }
     for (int e = t; e < MS::K * MS::GS; e += MS::NT) {
         const int q = e / MS::GS;
-        s[q * (MS::RUN + MS::GS) + MS::RUN + (e - q * MS::GS)] = KMAX<KEY>;
+        // ZW: the last of the GS words is the zero word below run q + 1
+        s[q * (MS::RUN + MS::GS) + MS::RUN + (e - q * MS::GS)] =
+            MS::ZW && e - q * MS::GS == MS::GS - 1 ? (KEY)0 : KMAX<KEY>;
     }
-    lds_barrier();
     int st[MS::K], ln[MS::K];
 #pragma unroll
     for (int q = 0; q < MS::K; ++q) {
         st[q] = q * (MS::RUN + MS::GS);
         ln[q] = MS::RUN;
     }
+    PairRec* pt = MS::PT ? reinterpret_cast<PairRec*>(s + MS::PT_AT) : nullptr;
+    lds_merge_prologue<KEY, MS>(s, st, ln, pt, t);
+    lds_barrier();
     KEY r[MS::RN];
     int ex = 0;
-    lds_merge_levels<KEY, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1);
+    lds_merge_levels<KEY, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1, pt);
     if (t * MS::IT < (1 << LT)) {
         if constexpr (MS::CH == 1 && MS::IT % 2 == 0) {
 #pragma unroll
@@ -631,7 +649,7 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
     constexpr int MF = sort_tile_mf<K, LT>();
     typedef SortMergeShape<K, LT, MF ? MF : 12> MS;
     // MERGE: 2 keys below the tile (a co-rank probe may read index -1; 16-byte alignment)
-    constexpr int WORDS = MF && MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T);
+    constexpr int WORDS = MF && MS::ALL_WORDS > lds_words(G::T) ? MS::ALL_WORDS : lds_words(G::T);
     __shared__ __attribute__((aligned(16))) K sbuf[WORDS + (MF ? 2 : 0)];
     K* s = MF ? sbuf + 2 : sbuf;
     const int t = threadIdx.x;
@@ -764,7 +782,8 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
     constexpr bool MERGE = MF > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
     typedef SortMergeShape<K, LT, MERGE ? MF : 12> MS;
     // MERGE: 4 words below the tile (a co-rank probe may read index -1)
-    __shared__ __attribute__((aligned(16))) K sbuf[(MERGE ? (MS::WORDS > lds_words(G::T) ? MS::WORDS : lds_words(G::T)) + 4
+    __shared__ __attribute__((aligned(16))) K sbuf[(MERGE ? (MS::ALL_WORDS > lds_words(G::T) ? MS::ALL_WORDS
+                                                                                               : lds_words(G::T)) + 4
                                                           : lds_words(G::T))];
     K* s = MERGE ? sbuf + 4 : sbuf;
     int64_t tile = tile0 + blockIdx.x;

@@ -66,7 +66,12 @@ __device__ __forceinline__ KEY lds_ld(uint32_t a) {
 #ifndef MISORT_MK_COR
 #define MISORT_MK_COR 2
 #endif
-template <typename KEY, int MAXR>
+// ZW (zero word): the word before every A sequence holds 0, a key <= every
+// key (and B[LB] is a sentinel), so the probe at lo holds through the data:
+// no i == lo test.  The probes then run on byte addresses of A (j = &A[i-1]; B's
+// probe at C - j), five VALU and two LDS reads per step instead of seven VALU,
+// an SALU or and two reads.
+template <typename KEY, int MAXR, bool ZW = false>
 __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr) {
     // first co-rank step: the largest power of two <= MAXR + PH (MAXR: a
     // compile-time bound on hi - lo, the steps must be powers of two for the
@@ -79,6 +84,24 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     const KEY* a = s + A0 - 1;
     const KEY* b = s + B0 + d;
     int base = lo - (PH ? (int)(__lane_id() & 31) : 0);
+    if constexpr (ZW && MISORT_MK_COR == 2) {
+        constexpr int W = (int)sizeof(KEY), WL = W == 4 ? 2 : 3;
+        const int ab = (int)lds_addr<KEY>(a);
+        const int C = ab + (int)lds_addr<KEY>(b);  // b[-i] at C - &a[i]
+        const int jlo = ab + (lo << WL), jhi = ab + (hi << WL);
+        int jb = ab + (base << WL);
+#pragma unroll
+        for (int step = CO_STEP0; step >= 1; step >>= 1) {
+            if (step > maxr + PH) continue;  // uniform
+            const int t = jb + (step << WL);
+            int j;
+            asm("v_med3_i32 %0, %1, %2, %3" : "=v"(j) : "v"(t), "v"(jlo), "v"(jhi));
+            const bool ok = lds_ld<KEY>((uint32_t)j) <= lds_ld<KEY>((uint32_t)(C - j));
+            jb = ok ? j : jb;
+        }
+        base = (jb - ab) >> WL;
+        return base > lo ? base : lo;
+    }
     if constexpr (MISORT_MK_COR == 2) {
         // every probe clamped into [lo, hi], both loads unconditional: a
         // probe at hi that holds makes hi the answer (later probes repeat
@@ -122,12 +145,12 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
 // one LDS read per output (u32).  Ties may go either way: equal keys are
 // identical.  Past the end of both sequences a chain outputs MAX (their
 // sentinels).
-template <typename KEY, int IT, int MAXR>
+template <typename KEY, int IT, int MAXR, bool ZW = false>
 __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
                                             KEY (&r)[IT]) {
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;  // lanes past the end: MAX outputs, in-bounds reads
-    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY, MAXR, ZW>(s, A0, LA, B0, LB, dc, maxr);
     // byte addresses of the two heads (LDS pointers are 32-bit)
     uint32_t px = lds_addr<KEY>(s + A0 + ia), py = lds_addr<KEY>(s + B0 + dc - ia);
     KEY h = lds_ld<KEY>(px), g = lds_ld<KEY>(py);
@@ -206,13 +229,13 @@ __device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
 // outputs (u32) -- the one-key chain spends six VALU and an LDS read per
 // output.  A side gives at most IT keys, so the G >= IT sentinels after each
 // sequence cover every read.
-template <typename KEY, int IT, bool WIDE, int MAXR>
+template <typename KEY, int IT, bool WIDE, int MAXR, bool ZW = false>
 __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
                                                 KEY (&r)[IT]) {
     static_assert(IT % 2 == 0, "two outputs per step");
     const int tot = LA + LB;
     const int dc = d < tot ? d : tot;
-    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
+    const int ia = co_rank<KEY, MAXR, ZW>(s, A0, LA, B0, LB, dc, maxr);
     constexpr uint32_t B2 = 2 * sizeof(KEY);
     const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
     const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
@@ -271,6 +294,83 @@ __device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int 
     return (ia & 1) + (ib & 1);
 }
 
+// Shape traits the level loop reads with defaults: ZW (a zero word before
+// every A sequence, co_rank without its i == lo test; requires a chain other
+// than 3 and G > the keys a chain reads past a sequence), PT (the level's pair
+// geometry from a table in LDS instead of per-pair selects).
+template <typename S, typename = void>
+struct shape_zw {
+    static constexpr bool v = false;
+};
+template <typename S>
+struct shape_zw<S, decltype((void)S::ZW)> {
+    static constexpr bool v = S::ZW;
+};
+template <typename S, typename = void>
+struct shape_pt {
+    static constexpr bool v = false;
+};
+template <typename S>
+struct shape_pt<S, decltype((void)S::PT)> {
+    static constexpr bool v = S::PT;
+};
+
+// Pair p of a level as the lanes read it from the pair table: A and B
+// (start, length), the output start and length; 8 ints per pair.
+struct PairRec {
+    int A0, LA, B0, LB, Q, LP, pad0, pad1;
+};
+
+// The pair geometry of a level of P pairs over sequences of lengths ln[]:
+// pair p's output starts at qp[p] (a multiple of QA past the previous pair's G
+// sentinels) and holds lp[p] keys; maxr bounds its co-rank range (uniform).
+template <typename S>
+__device__ __forceinline__ void level_geometry(const int* ln, int P, int (&qp)[S::K / 2], int (&lp)[S::K / 2],
+                                               int& maxr) {
+    int qa = 0;
+    maxr = 0;
+#pragma unroll
+    for (int p = 0; p < S::K / 2; ++p) {
+        if (p >= P) break;
+        const int mr = ln[2 * p] < ln[2 * p + 1] ? ln[2 * p] : ln[2 * p + 1];
+        maxr = mr > maxr ? mr : maxr;
+        lp[p] = ln[2 * p] + ln[2 * p + 1];
+        qp[p] = qa;
+        qa = (qa + lp[p] + S::G + S::QA - 1) / S::QA * S::QA;
+    }
+}
+
+// The pair table of a level of P pairs whose sequences are st[], ln[]: one
+// lane writes it (uniform values, three 8-byte writes per pair).
+template <typename S>
+__device__ __forceinline__ void write_pair_table(PairRec* pt, const int* st, const int* ln, int P, int tid) {
+    int qp[S::K / 2], lp[S::K / 2], maxr;
+    level_geometry<S>(ln, P, qp, lp, maxr);
+    if (tid == 0) {
+#pragma unroll
+        for (int p = 0; p < S::K / 2; ++p) {
+            if (p >= P) break;
+            int2* e = reinterpret_cast<int2*>(pt + p);
+            e[0] = int2{st[2 * p], ln[2 * p]};
+            e[1] = int2{st[2 * p + 1], ln[2 * p + 1]};
+            e[2] = int2{qp[p], lp[p]};
+        }
+    }
+}
+
+// Before the first level (the caller's barrier follows): for a ZW shape the
+// zero word below the first sequence (those between sequences are the
+// caller's: the last of the G words after each), and the first level's pair
+// table (pt: K / 2 records in LDS, or null).
+template <typename KEY, typename S>
+__device__ __forceinline__ void lds_merge_prologue(KEY* s, const int (&st)[S::K], const int (&ln)[S::K], PairRec* pt,
+                                                   int tid) {
+    if constexpr (shape_zw<S>::v) {
+        if (tid == 0) s[st[0] - 1] = (KEY)0;
+    }
+    if constexpr (shape_pt<S>::v && S::K > 2) write_pair_table<S>(pt, st, ln, S::K / 2, tid);
+}
+
 // The in-LDS levels: K sequences at st[q] (length ln[q], each followed by G
 // sentinels) merged pairwise in LK levels by NT lanes of IT outputs each.
 // Level lv writes pair p's output at qp[p] (a multiple of QA past the
@@ -279,13 +379,20 @@ __device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int 
 // of the merged sequence as r[ex, ex + IT).  S (a shape): K, LKS, NT, IT, G,
 // QA, RN (registers per lane: IT, or more for chains that merge extra keys),
 // CH (chain: 0 one key per read, 1/2 two, 3 aligned pairs), MAXR (bound on a
-// pair's shorter sequence).  MODE (probes): 1 = no merging, 2 = first level
-// only, 3 = co-rank searches without chains.  Ends with a barrier after the
-// last level's reads (the caller may then overwrite the LDS).
+// pair's shorter sequence), optionally ZW (shape_zw: G - 1 MAX sentinels and
+// a zero word after each sequence) and PT (shape_pt: the pair table pt).  MODE (probes): 1 = no merging, 2 = first
+// level only, 3 = co-rank searches without chains.  pt (null: per-pair
+// selects, (K/2 - 1) x 6 per lane): the pair table lds_merge_prologue wrote
+// for the first level; each level writes the next one's.  Ends with a barrier
+// after the last level's reads (the caller may then overwrite the LDS).
 template <typename KEY, typename S, int MODE>
 __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&ln)[S::K], KEY (&r)[S::RN], int& ex,
-                                                 int tid, int LAST) {
+                                                 int tid, int LAST, PairRec* pt = nullptr) {
     constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, RN = S::RN, CH = S::CH;
+    constexpr bool ZW = shape_zw<S>::v;
+    // a blk chain reads at most IT keys past a sequence, so the G-th word
+    // after it (G = IT + 1) is free for the next sequence's zero word
+    static_assert(!ZW || ((CH == 1 || CH == 2) && G > IT), "zero words: the two-key chains' sentinel layout");
     constexpr KEY MAXK = KMAX<KEY>;
     ex = 0;
     const int pos = tid * IT;
@@ -296,26 +403,41 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
         // pair p's output: [qp[p], qp[p] + lp[p]), then G sentinels; the next
         // pair starts at the first lane boundary past them
         int qp[K / 2], lp[K / 2];
-        int qa = 0, maxr = 0;  // maxr: the longest co-rank range of the level's pairs (uniform)
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const int mr = ln[2 * p] < ln[2 * p + 1] ? ln[2 * p] : ln[2 * p + 1];
-            maxr = mr > maxr ? mr : maxr;
-            lp[p] = ln[2 * p] + ln[2 * p + 1];
-            qp[p] = qa;
-            qa = (qa + lp[p] + G + S::QA - 1) / S::QA * S::QA;
-        }
+        int maxr;  // the longest co-rank range of the level's pairs (uniform)
+        level_geometry<S>(ln, P, qp, lp, maxr);
+        // uniform: the co-rank searches skip their long steps by scalar
+        // branches (a maxr the compiler left in a VGPR costs every step a
+        // compare and an exec-mask save / restore)
+        maxr = __builtin_amdgcn_readfirstlane(maxr);
         // the lane's pair: the last one starting at or before pos
         int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
+        if (P > 1) {
+            if constexpr (shape_pt<S>::v) {
+                int pi = 0;
 #pragma unroll
-        for (int p = 1; p < P; ++p) {
-            const bool in = pos >= qp[p];
-            A0 = in ? st[2 * p] : A0;
-            LA = in ? ln[2 * p] : LA;
-            B0 = in ? st[2 * p + 1] : B0;
-            LB = in ? ln[2 * p + 1] : LB;
-            Q = in ? qp[p] : Q;
-            LP = in ? lp[p] : LP;
+                for (int p = 1; p < K / 2; ++p)
+                    if (p < P) pi += pos >= qp[p] ? 1 : 0;
+                const int2* e = reinterpret_cast<const int2*>(pt + pi);
+                const int2 x = e[0], y = e[1], z = e[2];
+                A0 = x.x;
+                LA = x.y;
+                B0 = y.x;
+                LB = y.y;
+                Q = z.x;
+                LP = z.y;
+            } else {
+#pragma unroll
+                for (int p = 1; p < K / 2; ++p) {
+                    if (p >= P) break;
+                    const bool in = pos >= qp[p];
+                    A0 = in ? st[2 * p] : A0;
+                    LA = in ? ln[2 * p] : LA;
+                    B0 = in ? st[2 * p + 1] : B0;
+                    LB = in ? ln[2 * p + 1] : LB;
+                    Q = in ? qp[p] : Q;
+                    LP = in ? lp[p] : LP;
+                }
+            }
         }
         const int end = qp[P - 1] + lp[P - 1];
         if (MODE == 1 || (MODE == 2 && lv > 1) || MODE == 3) {
@@ -324,7 +446,7 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
             if (MODE == 3 && wpos < end) {  // the search alone, its result kept alive
                 const int dc = pos - Q < LA + LB ? pos - Q : LA + LB;
-                r[0] ^= (KEY)(co_rank<KEY, S::MAXR>(s, A0, LA, B0, LB, dc, maxr) & 1);
+                r[0] ^= (KEY)(co_rank<KEY, S::MAXR, ZW>(s, A0, LA, B0, LB, dc, maxr) & 1);
             }
         } else if (wpos < end) {
             if constexpr (CH == 0)
@@ -332,7 +454,7 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
             else if constexpr (CH == 3)
                 ex = merge_chain_al<KEY, IT, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else
-                merge_chain_blk<KEY, RN, CH == 2, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+                merge_chain_blk<KEY, RN, CH == 2, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         lds_barrier();
         if (lv < LK) {
@@ -351,16 +473,38 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                         *reinterpret_cast<kvec2<KEY>*>(s + pos + j) = kvec2<KEY>{r[j], r[j + 1]};
                 }
             }
-            for (int x = tid; x < P * G; x += NT) {
-                const int p = x / G;
+            // ZW: G - 1 MAX words after each output and a zero word below each
+            // pair's output but the first (the next level's A sequences start
+            // there; the one below the first was written once)
+            constexpr int GW = ZW ? G - 1 : G;
+            for (int x = tid; x < P * GW; x += NT) {
+                const int p = x / GW;
                 int e = 0;
 #pragma unroll
-                for (int q = 0; q < P; ++q) e = p == q ? qp[q] + lp[q] : e;
-                s[e + (x - p * G)] = MAXK;
+                for (int q = 0; q < K / 2; ++q)
+                    if (q < P) e = p == q ? qp[q] + lp[q] : e;
+                s[e + (x - p * GW)] = MAXK;
+            }
+            if constexpr (ZW) {
+                // the last wave's lanes 1 .. P-1 (its lanes past the sentinel loop's)
+                const int zl = tid - (NT - 64);
+                if (zl >= 1 && zl < P) {
+                    int e = 0;
+#pragma unroll
+                    for (int q = 1; q < K / 2; ++q)
+                        if (q < P) e = zl == q ? qp[q] : e;
+                    s[e - 1] = (KEY)0;
+                }
+            }
+            // the next level's pair table (its sequences: this level's
+            // outputs); every lane read this level's before the barrier above
+            if constexpr (shape_pt<S>::v) {
+                if ((P >> 1) > 1) write_pair_table<S>(pt, qp, lp, P >> 1, tid);
             }
             lds_barrier();
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
+            for (int p = 0; p < K / 2; ++p) {
+                if (p >= P) break;
                 st[p] = qp[p];
                 ln[p] = lp[p];
             }

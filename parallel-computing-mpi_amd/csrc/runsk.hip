@@ -87,6 +87,18 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_XCD
 #define MISORT_MK_XCD 0
 #endif
+#ifndef MISORT_MK_STAGGER
+#define MISORT_MK_STAGGER 0
+#endif
+#ifndef MISORT_MK_ZW
+#define MISORT_MK_ZW 1
+#endif
+#ifndef MISORT_MK_PT
+#define MISORT_MK_PT 0
+#endif
+#ifndef MISORT_MK_STAGGER_T
+#define MISORT_MK_STAGGER_T 5  // x 32 x 64 clocks ~ 4.3 us at 2.4 GHz
+#endif
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
 #endif
@@ -203,6 +215,10 @@ struct Shape {
     static constexpr int LS = ((IT + 1) & ~1) > LS_ROWS ? ((IT + 1) & ~1) : LS_ROWS;
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_KEYS = PAD + CAP + K * (G + QA) + 16;
+    // zero words below the A sequences (co_rank without its i == lo test) and
+    // the levels' pair table in LDS (MISORT_MK_ZW, MISORT_MK_PT)
+    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2);
+    static constexpr bool PT = MISORT_MK_PT && K > 2;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
@@ -924,7 +940,8 @@ __device__ __forceinline__ V out_vec(V v) {
 
 template <typename KEY, int LK, bool FENCES, int MODE, bool ORD = false>
 __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY* __restrict__ dst,
-                                             typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid) {
+                                             typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid,
+                                             PairRec* pt) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NT = S::NT, IT = S::IT;
     constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
@@ -941,7 +958,7 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
         st[q] = S::seg(d->o[q], q);
         ln[q] = d->o[q + 1] - d->o[q];
     }
-    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST);
+    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
     const int64_t out0 = d->out0;
     // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
@@ -986,16 +1003,28 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
     }
 }
 
-// The sentinels after every segment of the chunk.
+// The sentinels after every segment of the chunk (ZW: G - 1 of them and a
+// zero word, the word below the next segment), the zero word below the first
+// and the first level's pair table (pt).
 template <typename KEY, int LK>
-__device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d, int tid) {
+__device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d, int tid, PairRec* pt) {
     typedef Shape<KEY, LK> S;
     // a wave per segment (uniform segment index: the descriptor's offsets come
     // by scalar loads), G <= 64 lanes each
     static_assert(S::G <= 64, "sentinels: one wave per segment");
     const int lane = tid & 63;
     for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64)
-        if (lane < S::G) s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = KMAX<KEY>;
+        if (lane < S::G)
+            s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = S::ZW && lane == S::G - 1 ? (KEY)0 : KMAX<KEY>;
+    if constexpr (S::ZW || S::PT) {
+        int st[S::K], ln[S::K];
+#pragma unroll
+        for (int q = 0; q < S::K; ++q) {
+            st[q] = S::seg(d->o[q], q);
+            ln[q] = d->o[q + 1] - d->o[q];
+        }
+        lds_merge_prologue<KEY, S>(s, st, ln, pt, tid);
+    }
 }
 
 // k_mergek: one workgroup per chunk.  (A persistent grid that loads the next
@@ -1014,6 +1043,8 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
     __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
+    __shared__ PairRec ptab[S::PT ? S::K / 2 : 1];
+    PairRec* pt = S::PT ? ptab : nullptr;
     KEY* s = tile + PAD;
     const int tid = threadIdx.x;
     uint32_t chunk = blockIdx.x;
@@ -1024,6 +1055,18 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
         const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7, q = nb >> 3, rm = nb & 7;
         chunk = x * q + (x < rm ? x : rm) + (b >> 3);
     }
+#if MISORT_MK_STAGGER
+    // probe: the first resident round of workgroups starts staggered by a
+    // third of a chunk's time per CU slot, so a CU's workgroups do not load
+    // and merge in lockstep
+    if (blockIdx.x < 3u * 256u) {
+        uint32_t slot;
+        if (MISORT_MK_STAGGER == 1) slot = (__builtin_amdgcn_s_getreg(4 | (16 << 6) | (3 << 11))) % 3u;  // HW_ID.TG_ID
+        else if (MISORT_MK_STAGGER == 2) slot = (blockIdx.x >> 8) % 3u;
+        else slot = (blockIdx.x >> 3) % 3u;
+        for (uint32_t k = 0; k < slot * MISORT_MK_STAGGER_T; ++k) __builtin_amdgcn_s_sleep(32);
+    }
+#endif
     const Desc<KEY, LK>* d = desc + chunk;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
@@ -1060,10 +1103,10 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
             for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         }
-        mergek_sentinels<KEY, LK>(s, d, tid);
+        mergek_sentinels<KEY, LK>(s, d, tid, pt);
     }
     __syncthreads();
-    mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid);
+    mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid, pt);
 }
 
 // Fence buffers, bounds and descriptors: one grow-only set per (device, stream).
@@ -1241,9 +1284,10 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     if (lk_next > 0) {
         launch_timed(k_mergek<KEY, LK, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next);
-    } else if (sizeof(KEY) == 8 && ord_out) {
-        launch_timed(k_mergek<KEY, LK, false, 0, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
-                     (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
+    } else if (ord_out) {
+        if constexpr (sizeof(KEY) == 8)
+            launch_timed(k_mergek<KEY, LK, false, 0, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
+                         (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
     } else {
         launch_timed(k_mergek<KEY, LK, false>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
                      (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
