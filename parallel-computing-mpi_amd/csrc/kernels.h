@@ -106,6 +106,15 @@ template <typename K>
 hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out,
                        int keep_max, int64_t* scratch, hipStream_t s, LaunchHook* hook, bool ord_out = false);
 
+// The same compare-split IN PLACE when b touches one end of a: only the
+// affected window of a (found on the device: keep-min, a's keys after b[0];
+// keep-max, a's keys up to b[nb-1]) is staged into `stage` (same offsets) and
+// merged back; O(window + nb) instead of O(na).  scratch holds
+// ceil(na/2048) + 6 int64.
+template <typename K>
+hipError_t merge_split_tail(K* a, int64_t na, const K* b, int64_t nb, int keep_max, K* stage, int64_t* scratch,
+                            hipStream_t s, LaunchHook* hook);
+
 // Full merge of two ascending runs: out[0..na+nb) (A first on ties; for pure
 // keys the result equals std::sort of the concatenation).  scratch holds
 // ceil((na+nb)/2048)+1 int64 co-ranks.

@@ -137,6 +137,135 @@ __global__ __launch_bounds__(MS_NT) void k_merge_tiles(const K* __restrict__ A, 
     }
 }
 
+// ------------------------------------------------- in-place tail merge-split
+//
+// When the partner's k keys touch only one end of this rank's block, the
+// compare-split rewrites just that end, in place.  Keep-min (the block A
+// keeps its na smallest of A U B, B = the partner's bottom k keys): A's keys
+// up to and including B[0] stay where they are (A first on ties), so
+// out[0, p0) = A[0, p0), p0 = #{A[i] <= B[0]}, and out[p0, na) = the first
+// na - p0 of merge(A[p0, na), B).  Keep-max (B = the partner's top k): A's
+// keys after B[k-1] stay, out[q0, na) = A[q0, na), q0 = #{A[i] <= B[k-1]},
+// and out[0, q0) = merge positions [k, k + q0) of merge(A[0, q0), B).  The
+// window of A is staged first (a tile's writes would overwrite keys a later
+// tile still reads); then the window merges back into A through the usual
+// partition + LDS tiles, with sizes the device computed (the host knows k,
+// not the window): win = {window start in A, window length W, merge
+// diagonal offset}.  O(W + k) traffic instead of O(na): a 2^27-key block
+// with k = 4096 moved 0.2 ms of whole-block merge (profiles/r04 rank work).
+// The window: the first i with a[i] > x by a 1024-ary search (one workgroup,
+// 1024 probes per round: three rounds of loads for a 2^27-key block instead
+// of 27 dependent ones).
+constexpr int TW_NT = 1024;
+template <typename K>
+__global__ __launch_bounds__(TW_NT) void k_tail_window(const K* __restrict__ a, int64_t na, const K* __restrict__ b,
+                                                       int64_t nb, int keep_max, int64_t* __restrict__ win) {
+    int64_t w0 = 0, W = na;
+    if (nb > 0) {
+        const K x = keep_max ? b[nb - 1] : b[0];
+        int64_t lo = 0, hi = na;  // a[i] <= x for i < lo; the answer is in [lo, hi]
+        while (lo < hi) {
+            const int64_t step = (hi - lo + TW_NT - 1) / TW_NT;
+            const int64_t q = lo + (int64_t)threadIdx.x * step;
+            const int c = __syncthreads_count(q < hi && a[q] <= x);  // a prefix of the probes
+            if (step == 1) {
+                lo += c;
+                break;
+            }
+            const int64_t nlo = c > 0 ? lo + (int64_t)(c - 1) * step + 1 : lo;
+            const int64_t qc = lo + (int64_t)c * step;
+            hi = qc < hi ? qc : hi;
+            lo = nlo;
+        }
+        if (keep_max) {
+            W = lo;
+        } else {
+            w0 = lo;
+            W = na - lo;
+        }
+    }
+    if (threadIdx.x == 0) {
+        win[0] = w0;
+        win[1] = W;
+        win[2] = keep_max ? nb : 0;
+    }
+}
+
+template <typename K>
+__global__ void k_tail_stage(const K* __restrict__ a, K* __restrict__ st, const int64_t* __restrict__ win) {
+    const int64_t w0 = win[0], W = win[1];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < W; i += stride) st[w0 + i] = a[w0 + i];
+}
+
+template <typename K>
+__global__ void k_tail_partition(const K* __restrict__ st, const K* __restrict__ b, int64_t nb,
+                                 const int64_t* __restrict__ win, int64_t* __restrict__ co) {
+    const int64_t w0 = win[0], W = win[1], d0 = win[2];
+    const int64_t ntiles = (W + MS_TILE - 1) / MS_TILE;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles; t += stride) {
+        const int64_t off = t * MS_TILE < W ? t * MS_TILE : W;
+        co[t] = corank(st + w0, W, b, nb, d0 + off);
+    }
+}
+
+// The window's output tiles, a persistent grid walking them (the grid is
+// sized for the worst case W = na; most windows are a few tiles).
+template <typename K>
+__global__ __launch_bounds__(MS_NT) void k_tail_merge(const K* __restrict__ st, const K* __restrict__ b, int64_t nb,
+                                                      const int64_t* __restrict__ win, const int64_t* __restrict__ co,
+                                                      K* __restrict__ a, int keep_max) {
+    __shared__ K sh[MS_TILE];
+    const int64_t w0 = win[0], W = win[1], d0 = win[2];
+    const int64_t ntiles = (W + MS_TILE - 1) / MS_TILE;
+    const K* A = st + w0;
+    K* out = a + (keep_max ? 0 : w0);
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t ds = t * MS_TILE;
+        const int64_t de = (t + 1) * MS_TILE < W ? (t + 1) * MS_TILE : W;
+        const int64_t i0 = co[t], i1 = co[t + 1];
+        const int64_t j0 = d0 + ds - i0, j1 = d0 + de - i1;
+        const int la = (int)(i1 - i0), lb = (int)(j1 - j0), len = la + lb;
+        K x[MS_ITEMS];
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k) {
+            const int e = k * MS_NT + threadIdx.x;
+            const K* q = e < la ? A + i0 + e : b + j0 + (e - la);
+            x[k] = e < len ? *q : (K)0;
+        }
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k)
+            if (k * MS_NT + (int)threadIdx.x < len) sh[k * MS_NT + threadIdx.x] = x[k];
+        __syncthreads();
+        const int dk = threadIdx.x * MS_ITEMS < len ? threadIdx.x * MS_ITEMS : len;
+        int lo = dk - lb > 0 ? dk - lb : 0, hi = dk < la ? dk : la;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sh[mid] <= sh[la + dk - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+        }
+        int ia = lo, ib = dk - lo;
+        K r[MS_ITEMS];
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k) {
+            const K av = ia < la ? sh[ia] : KT<K>::MAX;
+            const K bv = ib < lb ? sh[la + ib] : KT<K>::MAX;
+            const bool takeA = ia < la && (ib >= lb || av <= bv);
+            r[k] = takeA ? av : bv;
+            ia += takeA;
+            ib += !takeA;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < MS_ITEMS; ++k)
+            if (dk + k < len) sh[dk + k] = r[k];
+        __syncthreads();
+        for (int k = threadIdx.x; k < len; k += MS_NT) out[ds + k] = sh[k];
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- helpers
 
 template <typename T>
@@ -288,6 +417,22 @@ hipError_t merge_split(const K* a, int64_t na, const K* b, int64_t nb, K* out, i
 }
 
 template <typename K>
+hipError_t merge_split_tail(K* a, int64_t na, const K* b, int64_t nb, int keep_max, K* stage, int64_t* scratch,
+                            hipStream_t s, LaunchHook* hook) {
+    if (na <= 0) return hipSuccess;
+    const int64_t ntiles = (na + MS_TILE - 1) / MS_TILE;  // the worst case, W = na
+    HookScope hs(hook, KIND_MERGE_SPLIT, (double)(2 * na + (nb < na ? nb : na)) * sizeof(K), s);
+    int64_t* win = scratch;
+    int64_t* co = scratch + 4;
+    k_tail_window<K><<<1, TW_NT, 0, s>>>(a, na, b, nb, keep_max, win);
+    k_tail_stage<K><<<stream_grid(na, 256), 256, 0, s>>>(a, stage, win);
+    const int64_t pg = (ntiles + 1 + 255) / 256;
+    k_tail_partition<K><<<(unsigned)(pg < 256 ? pg : 256), 256, 0, s>>>(stage, b, nb, win, co);
+    k_tail_merge<K><<<(unsigned)(ntiles < 1024 ? ntiles : 1024), MS_NT, 0, s>>>(stage, b, nb, win, co, a, keep_max);
+    return hipGetLastError();
+}
+
+template <typename K>
 hipError_t merge_full(const K* a, int64_t na, const K* b, int64_t nb, K* out, int64_t* scratch, hipStream_t s,
                       LaunchHook* hook) {
     const int64_t nout = na + nb;
@@ -372,6 +517,10 @@ template hipError_t merge_split<uint32_t>(const uint32_t*, int64_t, const uint32
                                           uint32_t*, int, int64_t*, hipStream_t, LaunchHook*, bool);
 template hipError_t merge_split<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t,
                                           uint64_t*, int, int64_t*, hipStream_t, LaunchHook*, bool);
+template hipError_t merge_split_tail<uint32_t>(uint32_t*, int64_t, const uint32_t*, int64_t, int, uint32_t*,
+                                               int64_t*, hipStream_t, LaunchHook*);
+template hipError_t merge_split_tail<uint64_t>(uint64_t*, int64_t, const uint64_t*, int64_t, int, uint64_t*,
+                                               int64_t*, hipStream_t, LaunchHook*);
 template hipError_t merge_full<uint32_t>(const uint32_t*, int64_t, const uint32_t*, int64_t, uint32_t*,
                                          int64_t*, hipStream_t, LaunchHook*);
 template hipError_t merge_full<uint64_t>(const uint64_t*, int64_t, const uint64_t*, int64_t, uint64_t*,

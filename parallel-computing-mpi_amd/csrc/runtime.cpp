@@ -784,6 +784,10 @@ struct misort_ctx {
     DevBuf relay_buf;
     // delta-coded exchange (codec.hip): MISORT_COMPRESS=0 / misort_set_compress(ctx, 0) disables
     bool compress = !getenv("MISORT_COMPRESS") || atoi(getenv("MISORT_COMPRESS")) != 0;
+    // a stage whose message is at most 1/tail_div of the block merges in place
+    // at the block's end (misort::merge_split_tail); 0 = always the
+    // whole-block merge (MISORT_TAIL_DIV)
+    int64_t tail_div = getenv("MISORT_TAIL_DIV") ? atoll(getenv("MISORT_TAIL_DIV")) : 8;
     DevBuf enc_send, enc_recv, codec_scr;
     int64_t xchg_raw_bytes = 0;  // what the coded stages would have moved uncoded
     ~misort_ctx() {
@@ -889,6 +893,25 @@ int do_merge_split(misort_ctx* c, int dtype, const void* a, int64_t na, const vo
         e = misort::merge_split<uint64_t>((const uint64_t*)a, na, (const uint64_t*)b, nb,
                                           (uint64_t*)out, keep_max, (int64_t*)c->scratch.p, s, hook(c), ord_out);
     if (e != hipSuccess) return fail(MISORT_E_HIP, "merge_split: %s", hipGetErrorString(e));
+    return MISORT_OK;
+}
+
+// The compare-split in place in `a` (psort.cc:116-164 keep-n semantics): only
+// the end of the block the k received keys reach is rewritten, staged through
+// `stage` (a block-sized buffer).
+int do_merge_split_tail(misort_ctx* c, int dtype, void* a, int64_t na, const void* b, int64_t nb, void* stage,
+                        int keep_max, hipStream_t s) {
+    const int64_t ntiles = (na + 2047) / 2048 + 6;
+    int rc = c->scratch.ensure((size_t)ntiles * sizeof(int64_t));
+    if (rc) return rc;
+    hipError_t e;
+    if (dtype == MISORT_U32)
+        e = misort::merge_split_tail<uint32_t>((uint32_t*)a, na, (const uint32_t*)b, nb, keep_max, (uint32_t*)stage,
+                                               (int64_t*)c->scratch.p, s, hook(c));
+    else
+        e = misort::merge_split_tail<uint64_t>((uint64_t*)a, na, (const uint64_t*)b, nb, keep_max, (uint64_t*)stage,
+                                               (int64_t*)c->scratch.p, s, hook(c));
+    if (e != hipSuccess) return fail(MISORT_E_HIP, "merge_split_tail: %s", hipGetErrorString(e));
     return MISORT_OK;
 }
 
@@ -1253,6 +1276,11 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                 continue;
             }
             xg_close((double)(c->xchg_bytes - moved0));
+            if (c->tail_div > 0 && k * c->tail_div <= loc) {
+                // a small bracket: rewrite only the end of the block it reaches
+                if ((rc = do_merge_split_tail(c, dtype, cur, loc, rkeys, k, other, keep[st], s))) return rc;
+                continue;
+            }
             // the last stage, writing `out`: f64 bits straight from the merge
             const bool oo = f64 && st == nst - 1 && other == out;
             if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, k, other, keep[st], s, oo))) return rc;
@@ -1305,6 +1333,10 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         c->xchg_bytes += (int64_t)(sbytes + rbytes);
         c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
         xg_close((double)(c->xchg_bytes - moved0));
+        if (k > 0 && c->tail_div > 0 && k * c->tail_div <= loc) {
+            if ((rc = do_merge_split_tail(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
+            continue;
+        }
         const bool oo = f64 && st == nst - 1 && other == out;
         if ((rc = do_merge_split(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s, oo))) return rc;
         ord_done = ord_done || oo;
@@ -1909,8 +1941,18 @@ int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc
     if (!c || !valid_dtype(dtype) || nloc < 0 || nrecv < 0)
         return fail(MISORT_E_INVALID, "bad merge_split arguments");
     hipStream_t s = pick(c, stream);
-    if (dtype != MISORT_F64)
+    if (dtype != MISORT_F64) {
+        // MISORT_MERGE_SPLIT_TAIL=1 (tests): the in-place tail merge the
+        // hypercube stages use for small brackets, on a copy of local in out
+        const char* tail = getenv("MISORT_MERGE_SPLIT_TAIL");
+        if (tail && atoi(tail) != 0 && nloc > 0) {
+            int rc = c->work.ensure((size_t)nloc * key_bytes(dtype));
+            if (rc) return rc;
+            if (out != local) HIPCHK(hipMemcpyAsync(out, local, (size_t)nloc * key_bytes(dtype), hipMemcpyDeviceToDevice, s));
+            return do_merge_split_tail(c, dtype, out, nloc, recv, nrecv, c->work.p, keep_max, s);
+        }
         return do_merge_split(c, dtype, local, nloc, recv, nrecv, out, keep_max, s);
+    }
     // f64: order-preserving copies of both blocks, merge, map back.
     int rc;
     if ((rc = c->work.ensure(std::max<size_t>(8, (size_t)nloc * 8)))) return rc;

@@ -128,6 +128,41 @@ def test_merge_split(ctx, na, nb, keep_max):
     np.testing.assert_array_equal(to_host(out, np.uint32), want)
 
 
+@pytest.mark.parametrize("case", ["tail", "head", "overlap", "dups", "wide"])
+@pytest.mark.parametrize("na,nb", [(1, 1), (4097, 3), (100000, 4096), (1 << 20, 777)])
+@pytest.mark.parametrize("keep_max", [0, 1])
+@pytest.mark.parametrize("kd", [np.uint32, np.uint64])
+def test_merge_split_tail(ctx, monkeypatch, case, na, nb, keep_max, kd):
+    """The in-place compare-split of a small bracket (merge_split_tail: only
+    the end of the block the partner's keys reach is rewritten) against the
+    oracle's keep-n merge (psort.cc:116-164).  The partner's keys sit at the
+    block's far end (tail: the usual small-bracket stage), straddle all of it
+    (wide: the window is the whole block), duplicate its boundary keys, or
+    overlap its middle."""
+    monkeypatch.setenv("MISORT_MERGE_SPLIT_TAIL", "1")
+    big = 1 << 30 if kd == np.uint32 else 1 << 60
+    a = O.local_sort((O.splitmix(na * 5 + 2, na, np.uint64) % big).astype(kd))
+    r = O.splitmix(nb * 3 + 9, nb, np.uint64)
+    if case == "tail":  # keep-min receives keys above most of a; keep-max, below most of it
+        lo = int(a[max(0, na - 3 * nb)]) if not keep_max else 0
+        hi = int(a[-1]) + 1000 if not keep_max else int(a[min(na - 1, 3 * nb)])
+    elif case == "head":  # the other end: the window is (nearly) the whole block
+        lo, hi = (0, int(a[min(na - 1, 2)]) + 1) if not keep_max else (int(a[max(0, na - 3)]), big)
+    elif case == "wide":
+        lo, hi = 0, big
+    elif case == "overlap":
+        lo, hi = int(a[na // 3]), int(a[(2 * na) // 3]) + 1
+    else:  # dups: b repeats a's keys at the boundary
+        idx = (r % max(1, min(na, 8))).astype(np.int64)
+        b = O.local_sort(a[(na - 1 - idx) if not keep_max else idx].astype(kd))
+        lo = hi = None
+    if lo is not None:
+        b = O.local_sort((lo + r % max(1, hi - lo)).astype(kd))
+    want = O.compare_split(a, b, keep_max)
+    out = ctx.compare_split(to_dev(a), to_dev(b), keep_max)
+    np.testing.assert_array_equal(to_host(out, kd), want)
+
+
 @pytest.mark.parametrize("keep_max", [0, 1])
 def test_merge_split_f64(ctx, keep_max):
     a = O.local_sort(O.generate_f64(5001))

@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--p", type=int, default=8)
     ap.add_argument("--dtype", choices=["u32", "u64"], default="u32")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tail-div", type=int, default=8, help="the runtime rule: k * tail_div <= block -> in-place tail merge")
     a = ap.parse_args()
     n = a.n or (1 << a.logn)
     p = a.p
@@ -121,9 +122,11 @@ def main():
     torch.full((1,), 7, device="cuda").add_(1)
     torch.cuda.synchronize()
 
-    def timed(fn):
+    def timed(fn, setup=None):
         ms = []
         for _ in range(a.reps + 1):
+            if setup:
+                setup()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             fn()
@@ -148,11 +151,27 @@ def main():
             row.update(encode_ms=enc_ms, decode_ms=dec_ms, coded_bytes=nbytes, raw_bytes=k * w,
                        codec_ok=bool(torch.equal(dec, x["recv"])))
             mo = torch.empty_like(x["mine"])
-            t = timed(lambda: ctx.compare_split(x["mine"], x["recv"], x["keep_max"], out=mo))
             # merge-split bytes: read n_me + k, write n_me
             mb = (2 * x["n_me"] + k) * w
-            row.update(merge_split_ms=t, merge_split_bytes=mb, merge_split_TBs=mb / (t * 1e-3) / 1e12,
-                       merge_split_frac=mb / (t * 1e-3) / 8e12)
+            if k * a.tail_div <= x["n_me"]:
+                # the runtime's small-bracket path: in place at the block's end
+                # (merge_split_tail); the block is restored before each rep
+                os.environ["MISORT_MERGE_SPLIT_TAIL"] = "1"
+                t = timed(lambda: ctx.compare_split(mo, x["recv"], x["keep_max"], out=mo),
+                          setup=lambda: mo.copy_(x["mine"]))
+                os.environ.pop("MISORT_MERGE_SPLIT_TAIL")
+                mine, rv = x["mine"], x["recv"]
+                if x["keep_max"]:
+                    win = int(torch.searchsorted(mine, rv[-1:], right=True).item())
+                else:
+                    win = x["n_me"] - int(torch.searchsorted(mine, rv[:1], right=True).item())
+                tb = (3 * win + k) * w  # stage the window, read it and the k keys, write it back
+                row.update(merge_split_path="tail (in place)", tail_window=win, merge_split_ms=t,
+                           merge_split_window_bytes=tb, merge_split_bytes=mb)
+            else:
+                t = timed(lambda: ctx.compare_split(x["mine"], x["recv"], x["keep_max"], out=mo))
+                row.update(merge_split_path="whole block", merge_split_ms=t, merge_split_bytes=mb,
+                           merge_split_TBs=mb / (t * 1e-3) / 1e12, merge_split_frac=mb / (t * 1e-3) / 8e12)
         rows.append(row)
     res["stages"] = rows
     dev = res["local_sort"]["ms"] + sum(r.get("encode_ms", 0) + r.get("decode_ms", 0) + r.get("merge_split_ms", 0)

@@ -46,9 +46,13 @@ if len(sys.argv) > 2:
         if r["k"] == 0:
             print(f"stage {r['stage']}: partner {r['partner']}, k = 0 (skipped)")
             continue
+        if r.get("merge_split_path", "whole block") == "whole block":
+            ms = (f"merge-split {r['merge_split_ms']:.3f} ms = {r['merge_split_TBs']:.2f} TB/s "
+                  f"(frac {r['merge_split_frac']:.3f} of 8 TB/s)")
+        else:
+            ms = (f"merge-split in place at the block's end {r['merge_split_ms']:.3f} ms (window "
+                  f"{r['tail_window']} keys, {r['merge_split_window_bytes'] / 1e6:.2f} MB moved)")
         print(f"stage {r['stage']}: partner {r['partner']} keep_max {r['keep_max']} k = {r['k']} "
               f"({r['k'] / r['n_partner']:.3f} of the block): encode {r['encode_ms']:.3f} + decode "
-              f"{r['decode_ms']:.3f} ms (coded {r['coded_bytes'] / max(1, r['raw_bytes']):.3f} of raw), "
-              f"merge-split {r['merge_split_ms']:.3f} ms = {r['merge_split_TBs']:.2f} TB/s "
-              f"(frac {r['merge_split_frac']:.3f} of 8 TB/s)")
+              f"{r['decode_ms']:.3f} ms (coded {r['coded_bytes'] / max(1, r['raw_bytes']):.3f} of raw), " + ms)
     print(f"device work per sort (rank 0): {pr['device_ms_per_sort']:.3f} ms")
