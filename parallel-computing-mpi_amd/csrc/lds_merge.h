@@ -390,9 +390,10 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                                                  int tid, int LAST, PairRec* pt = nullptr) {
     constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, RN = S::RN, CH = S::CH;
     constexpr bool ZW = shape_zw<S>::v;
-    // a blk chain reads at most IT keys past a sequence, so the G-th word
-    // after it (G = IT + 1) is free for the next sequence's zero word
-    static_assert(!ZW || ((CH == 1 || CH == 2) && G > IT), "zero words: the two-key chains' sentinel layout");
+    // a blk chain reads at most IT keys past a sequence (the one-key chain
+    // IT + 1), so the G-th word after it is free for the next sequence's zero word
+    static_assert(!ZW || ((CH == 1 || CH == 2) && G > IT) || (CH == 0 && G > IT + 1),
+                  "zero words: a sentinel word past the chain's reads");
     constexpr KEY MAXK = KMAX<KEY>;
     ex = 0;
     const int pos = tid * IT;
@@ -450,7 +451,7 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
             }
         } else if (wpos < end) {
             if constexpr (CH == 0)
-                merge_chain<KEY, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+                merge_chain<KEY, RN, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else if constexpr (CH == 3)
                 ex = merge_chain_al<KEY, IT, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else

@@ -87,17 +87,12 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_XCD
 #define MISORT_MK_XCD 0
 #endif
-#ifndef MISORT_MK_STAGGER
-#define MISORT_MK_STAGGER 0
-#endif
 #ifndef MISORT_MK_ZW
 #define MISORT_MK_ZW 1
 #endif
+
 #ifndef MISORT_MK_PT
 #define MISORT_MK_PT 0
-#endif
-#ifndef MISORT_MK_STAGGER_T
-#define MISORT_MK_STAGGER_T 5  // x 32 x 64 clocks ~ 4.3 us at 2.4 GHz
 #endif
 #ifndef MISORT_MK_GLDS
 #define MISORT_MK_GLDS 1
@@ -197,7 +192,12 @@ struct Shape {
     // after up to two early keys) and reads up to RN + 2 - 2 keys past a
     // sequence start; chains 0-2 read up to IT
     static constexpr int RN = CH == 3 ? (IT + 3) & ~1 : IT;
-    static constexpr int G = CH == 3 ? RN + 1 : IT + 1;
+    // zero words below the A sequences (co_rank without its i == lo test;
+    // MISORT_MK_ZW): the last of the G words after a sequence holds the next
+    // one's, so G exceeds the keys a chain reads past a sequence (IT for the
+    // two-key chains, IT + 1 for the one-key chain)
+    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2);
+    static constexpr int G = CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
     // level outputs start at lane boundaries; chain 3 also needs even slots
     static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
     static_assert(CH != 3 || QA % 2 == 0, "chain 3: even sequence starts");
@@ -215,9 +215,7 @@ struct Shape {
     static constexpr int LS = ((IT + 1) & ~1) > LS_ROWS ? ((IT + 1) & ~1) : LS_ROWS;
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
     static constexpr int LDS_KEYS = PAD + CAP + K * (G + QA) + 16;
-    // zero words below the A sequences (co_rank without its i == lo test) and
-    // the levels' pair table in LDS (MISORT_MK_ZW, MISORT_MK_PT)
-    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2);
+    // the levels' pair table in LDS (MISORT_MK_PT)
     static constexpr bool PT = MISORT_MK_PT && K > 2;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
@@ -1055,18 +1053,6 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
         const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7, q = nb >> 3, rm = nb & 7;
         chunk = x * q + (x < rm ? x : rm) + (b >> 3);
     }
-#if MISORT_MK_STAGGER
-    // probe: the first resident round of workgroups starts staggered by a
-    // third of a chunk's time per CU slot, so a CU's workgroups do not load
-    // and merge in lockstep
-    if (blockIdx.x < 3u * 256u) {
-        uint32_t slot;
-        if (MISORT_MK_STAGGER == 1) slot = (__builtin_amdgcn_s_getreg(4 | (16 << 6) | (3 << 11))) % 3u;  // HW_ID.TG_ID
-        else if (MISORT_MK_STAGGER == 2) slot = (blockIdx.x >> 8) % 3u;
-        else slot = (blockIdx.x >> 3) % 3u;
-        for (uint32_t k = 0; k < slot * MISORT_MK_STAGGER_T; ++k) __builtin_amdgcn_s_sleep(32);
-    }
-#endif
     const Desc<KEY, LK>* d = desc + chunk;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
