@@ -11,10 +11,15 @@ namespace misort {
 
 // IEEE double bits <-> order-preserving u64 (negative: all bits flipped; else
 // the sign bit set), so every kernel compares unsigned integers.
+#ifndef MISORT_ORD_NOP
+#define MISORT_ORD_NOP 0  // probe builds only: no mapping (wrong for negative doubles)
+#endif
 __device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
+    if (MISORT_ORD_NOP) return b;
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 __device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
+    if (MISORT_ORD_NOP) return o;
     return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
 }
 
