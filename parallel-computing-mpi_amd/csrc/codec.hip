@@ -32,6 +32,36 @@ constexpr int SCN = 1024;                         // blocks per chunk of the pay
 
 __device__ __forceinline__ int width_of(uint64_t d) { return d ? 64 - __builtin_clzll(d) : 0; }
 
+// The lane's keys j0-1 .. j0+CI-1 (x[0] = the key before its run, unread at
+// the block start): one 4-byte-aligned vector load of its CI keys (the run's
+// start is any key offset) instead of a load per key and per predecessor.
+template <typename K>
+__device__ __forceinline__ void lane_keys(const K* __restrict__ keys, int64_t j0, int64_t k0, int64_t n,
+                                          K (&x)[CI + 1]) {
+    static_assert(CI == 4, "4-key lane runs");
+    if (j0 + CI <= n) {
+        if constexpr (sizeof(K) == 4) {
+            typedef uint32_t v4 __attribute__((ext_vector_type(4), aligned(4)));
+            const v4 v = *reinterpret_cast<const v4*>(keys + j0);
+            x[1] = v.x;
+            x[2] = v.y;
+            x[3] = v.z;
+            x[4] = v.w;
+        } else {
+            typedef uint64_t v2 __attribute__((ext_vector_type(2), aligned(8)));
+            const v2 a = *reinterpret_cast<const v2*>(keys + j0), b = *reinterpret_cast<const v2*>(keys + j0 + 2);
+            x[1] = a.x;
+            x[2] = a.y;
+            x[3] = b.x;
+            x[4] = b.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < CI; ++i) x[i + 1] = j0 + i < n ? keys[j0 + i] : (K)0;
+    }
+    x[0] = j0 > k0 && j0 - 1 < n ? keys[j0 - 1] : (K)0;
+}
+
 // Per block: payload words for its gaps at the block's width.  (Lane-strided
 // loads of 4 consecutive keys; measured faster here than coalesced loads with a
 // cross-lane predecessor, and than packing through LDS atomics.)  The run is
@@ -52,10 +82,12 @@ __global__ __launch_bounds__(CT) void k_codec_width(const K* __restrict__ base, 
         return;
     }
     uint64_t mx = 0;
+    K x[CI + 1];  // keys j-1 .. j+3 of the lane's 4-key run j = k0 + 4t
+    lane_keys<K>(keys, k0 + (int64_t)t * CI, k0, n, x);
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
         const int64_t j = k0 + t * CI + i;  // gap: key j minus key j-1
-        if (j > k0 && j < n) mx = max(mx, (uint64_t)(keys[j] - keys[j - 1]));
+        if (j > k0 && j < n) mx = max(mx, (uint64_t)(x[i + 1] - x[i]));
     }
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, o));
     if ((t & 63) == 0) red[t >> 6] = mx;
@@ -137,10 +169,17 @@ __global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ kbase, 
     const int64_t nblk = (n + CB - 1) / CB;
     const int t = threadIdx.x;
     const int64_t cnt = n - k0 < CB ? n - k0 : CB;
+    {
+        // gap j (key k0+j+1 minus key k0+j) from the lane's run of keys
+        // k0+4t .. k0+4t+3 and the key before it: gap 4t-1+i = x[i+1] - x[i]
+        K x[CI + 1];
+        lane_keys<K>(keys, k0 + (int64_t)t * CI, k0, k0 + cnt, x);
 #pragma unroll
-    for (int i = 0; i < CI; ++i) {
-        const int j = t * CI + i;  // gap j: key k0+j+1 minus key k0+j
-        gap[j] = (j + 1 < cnt) ? (uint64_t)(keys[k0 + j + 1] - keys[k0 + j]) : 0;
+        for (int i = 0; i < CI; ++i) {
+            const int j = t * CI + i - 1;
+            if (j >= 0) gap[j] = (j + 1 < cnt) ? (uint64_t)(x[i + 1] - x[i]) : 0;
+        }
+        if (t == CT - 1) gap[CB - 1] = 0;
     }
     __syncthreads();
     const int w = wid[b];
@@ -181,6 +220,9 @@ __global__ __launch_bounds__(CT) void k_codec_unpack(const uint32_t* __restrict_
                                                      K* __restrict__ keys) {
     static_assert(CI == 4, "one 4-key run per lane");
     __shared__ uint64_t wsum[CT / 64];
+    // the block's payload words, staged by coalesced loads (each lane's bit
+    // fields then read LDS instead of up to three scattered global words per key)
+    __shared__ uint32_t pay[(CB * 64 + 31) / 32 + 2];
     const int64_t b = blockIdx.x, k0 = b * CB;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t cnt = n - k0 < CB ? n - k0 : CB;
@@ -189,6 +231,10 @@ __global__ __launch_bounds__(CT) void k_codec_unpack(const uint32_t* __restrict_
     const uint32_t pw = h[2];
     const int w = (int)h[3];
     const uint64_t mask = w >= 64 ? ~0ull : ((1ull << w) - 1);
+    const int nw = (int)(((cnt - 1) * w + 31) >> 5);
+    for (int q = t; q < nw; q += CT) pay[q] = in[pw + q];
+    if (t < 2) pay[nw + t] = 0u;  // a field's read of the words past the payload
+    __syncthreads();
     uint64_t g[CI], s = 0;
 #pragma unroll
     for (int i = 0; i < CI; ++i) {
@@ -196,7 +242,7 @@ __global__ __launch_bounds__(CT) void k_codec_unpack(const uint32_t* __restrict_
         uint64_t f = 0;
         if (w && j >= 0 && j + 1 < cnt) {
             const int64_t bit = j * w;
-            const uint32_t* p = in + pw + (bit >> 5);
+            const uint32_t* p = pay + (bit >> 5);
             const int sh = (int)(bit & 31);
             const uint64_t lo = (uint64_t)p[0] | ((uint64_t)(sh + w > 32 ? p[1] : 0) << 32);
             f = lo >> sh;
