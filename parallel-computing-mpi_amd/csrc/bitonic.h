@@ -517,6 +517,9 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_ZW
 #define MISORT_SORT_ZW 1
 #endif
+#ifndef MISORT_SORT_CH_U64
+#define MISORT_SORT_CH_U64 0
+#endif
 #ifndef MISORT_SORT_PT
 #define MISORT_SORT_PT 0
 #endif
@@ -525,12 +528,13 @@ struct SortMergeShape {
     static_assert(F >= 7 && F <= 12 && F <= LT, "merge levels from runs of 64 .. 2^11 keys");
     static constexpr int NT = 1 << (LT - 5);  // 32 keys per lane
     static constexpr int K = 1 << (LT - F + 1), LKS = LT - F + 1, RUN = 1 << (F - 1);
-    static constexpr int CH = sizeof(KEY) == 4 ? 1 : 0;  // two-key chains for u32, one key per read for u64
+    // two-key chains for u32, one key per read for u64 (MISORT_SORT_CH_U64)
+    static constexpr int CH = sizeof(KEY) == 4 ? 1 : MISORT_SORT_CH_U64;
     // outputs per lane: the smallest count from IT0 up (step 2) whose level
     // layouts fit: 2^LT keys + per pair G + QA gap.  u32: even (IT0 = 34),
     // so every level writes aligned pairs; u64: odd (33: lanes' diagonals on
     // distinct banks; a pair of u64 keys is a 16-byte write, no cheaper than two)
-    static constexpr int IT0 = CH == 1 ? MISORT_SORT_IT0 : 33;
+    static constexpr int IT0 = CH == 1 ? (sizeof(KEY) == 4 ? MISORT_SORT_IT0 : 32) : 33;
     static constexpr int rn(int it) { return CH == 1 ? (it + 1) & ~1 : it; }
     static constexpr int fit(int it) {
         return (1 << LT) + (K / 2) * (rn(it) + 1 + it) <= NT * it ? it : fit(it + 2);
