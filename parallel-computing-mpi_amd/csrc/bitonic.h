@@ -275,6 +275,80 @@ __device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
     }
 }
 
+// Levels 1..5 of the tile: the 32 register keys of a lane into ascending
+// order.  MISORT_SORT_OEM: Batcher's odd-even merge sort (191 compare-exchanges
+// in the same 15 steps) instead of the bitonic stages (240); the steps after
+// it only need each lane's 32 keys ascending.
+#ifndef MISORT_SORT_OEM
+#define MISORT_SORT_OEM 1
+#endif
+// One step (P, D) of the odd-even merge sort: the pairs (i, i + D) inside
+// one 2P-block, in runs of D starting at D mod P.
+template <typename K, int P, int D>
+__device__ __forceinline__ void oem_step(K (&v)[32]) {
+    if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP && MISORT_CX64_BATCH) {
+        // u64: the step's compares first, then the selects (as reg_stages_c)
+        bool lt[16];
+        int q = 0;
+#pragma unroll
+        for (int j = D % P; j + D < 32; j += 2 * D)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (i + j + D < 32 && (i + j) / (2 * P) == (i + j + D) / (2 * P)) lt[q++] = v[i + j] < v[i + j + D];
+#pragma unroll
+        for (int j = D % P; j + D < 32; j += 2 * D)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (i + j + D < 32 && (i + j) / (2 * P) == (i + j + D) / (2 * P))
+                    asm("" : "+v"(v[i + j]), "+v"(v[i + j + D]));
+        q = 0;
+#pragma unroll
+        for (int j = D % P; j + D < 32; j += 2 * D)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (i + j + D < 32 && (i + j) / (2 * P) == (i + j + D) / (2 * P)) {
+                    K& a = v[i + j];
+                    K& b = v[i + j + D];
+                    const bool l = lt[q++];
+                    const K lo = l ? a : b, hi = l ? b : a;
+                    a = lo;
+                    b = hi;
+                }
+    } else {
+#pragma unroll
+        for (int j = D % P; j + D < 32; j += 2 * D)
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+                if (i + j + D < 32 && (i + j) / (2 * P) == (i + j + D) / (2 * P)) cx(v[i + j], v[i + j + D]);
+    }
+}
+template <typename K>
+__device__ __forceinline__ void sort32_regs(K (&v)[32]) {
+    if constexpr (MISORT_SORT_OEM) {
+        oem_step<K, 1, 1>(v);
+        oem_step<K, 2, 2>(v);
+        oem_step<K, 2, 1>(v);
+        oem_step<K, 4, 4>(v);
+        oem_step<K, 4, 2>(v);
+        oem_step<K, 4, 1>(v);
+        oem_step<K, 8, 8>(v);
+        oem_step<K, 8, 4>(v);
+        oem_step<K, 8, 2>(v);
+        oem_step<K, 8, 1>(v);
+        oem_step<K, 16, 16>(v);
+        oem_step<K, 16, 8>(v);
+        oem_step<K, 16, 4>(v);
+        oem_step<K, 16, 2>(v);
+        oem_step<K, 16, 1>(v);
+    } else {
+        reg_stages_c<K, 0, 1, true>(v);
+        reg_stages_c<K, 1, 2, true>(v);
+        reg_stages_c<K, 2, 3, true>(v);
+        reg_stages_c<K, 3, 4, true>(v);
+        reg_stages_c<K, 4, 5, true>(v);
+    }
+}
+
 // One LDS phase, window [B, B+5) of the virtual index, compile-time shape.
 template <typename K, int B, int TOP, int CNT, bool FLIP>
 __device__ __forceinline__ void phase_c(K* s, int t) {
@@ -688,11 +762,7 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
                 for (int c = 0; c < 32; ++c)
                     if (full || v0 + c < n) v[c] = (K)ord_of_f64((uint64_t)v[c]);
             }
-            reg_stages_c<K, 0, 1, true>(v);
-            reg_stages_c<K, 1, 2, true>(v);
-            reg_stages_c<K, 2, 3, true>(v);
-            reg_stages_c<K, 3, 4, true>(v);
-            reg_stages_c<K, 4, 5, true>(v);
+            sort32_regs<K>(v);
 #pragma unroll
             for (int c = 0; c < 32; ++c) s[a0 + c] = v[c];
         }
@@ -824,11 +894,7 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
             uint32_t x[32];
 #pragma unroll
             for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
-            reg_stages_c<uint32_t, 0, 1, true>(x);
-            reg_stages_c<uint32_t, 1, 2, true>(x);
-            reg_stages_c<uint32_t, 2, 3, true>(x);
-            reg_stages_c<uint32_t, 3, 4, true>(x);
-            reg_stages_c<uint32_t, 4, 5, true>(x);
+            sort32_regs<uint32_t>(x);
             wave_levels<6, WL>(x, t & 63);
             // each lane rewrites only the keys it read: no barrier before, and the
             // next phase (level WL+1 <= 11) stays inside the wave
