@@ -1101,11 +1101,12 @@ struct Scratch {
     size_t bytes = 0;
 };
 std::mutex g_mu;
-std::map<std::pair<int, hipStream_t>, Scratch> g_scr[2];
+std::map<std::pair<int, hipStream_t>, Scratch> g_scr[4];
 
 // which = 0: the two fence buffers (a pass's input fences are the previous
 // pass's output: sized by n alone, so they never move between the passes of
-// one sort); which = 1: per-pass planning data (free to grow at any pass).
+// one sort); which = 1: per-pass planning data (free to grow at any pass);
+// 2 and 3: the same for a pass nested in a pass's fence merge (depth 1).
 void* scratch(int which, size_t bytes, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -1144,9 +1145,22 @@ int64_t chunks_of(const Geo& geo) {
     return geo.nfull * geo.kf + (tail ? geo.nchunks(geo.nfull) : 0);
 }
 
+// The fence merge levels of a u32 pass as one multi-way merge pass over the
+// fences themselves (u64 keys, depth 1) once at least FENCE_NEST_LEVELS of
+// them would run as global 2-way merge levels and the pass has at least
+// 2^MISORT_FENCE_NEST_MIN fences (env; 0 = never): one HBM sweep of the fence
+// array instead of one per level.  Measured (profiles/r05/plan/nest_ab.txt):
+// 2^30 u32 passes 3 and 4 (2^23 fences) -30 us each, +0.6 %; at 2^22 fences
+// (2^29 keys) the nested pass's ~600 chunks underfill the chip: +5 us, so the
+// default threshold is 2^23.
+#ifndef MISORT_FENCE_NEST
+#define MISORT_FENCE_NEST 1
+#endif
+constexpr int FENCE_NEST_LEVELS = 3;
+
 template <typename KEY, int LK>
 hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s, int phase, bool gather,
-                      int lk_next, LaunchHook* hook, bool ord_out) {
+                      int lk_next, LaunchHook* hook, bool ord_out, int depth = 0) {
     typedef Shape<KEY, LK> S;
     typedef typename KTr<KEY>::F FT;
     const Geo geo = make_geo<KEY>(n, lw, LK);
@@ -1166,8 +1180,8 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const size_t bb = ((size_t)nslots * S::K * 8 + 255) & ~(size_t)255;
     const size_t cb = ((size_t)nbk * cpb * S::K * 4 + 255) & ~(size_t)255;
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
-    char* fbase = (char*)scratch(0, 2 * fb, s);
-    char* base = (char*)scratch(1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
+    char* fbase = (char*)scratch(2 * depth, 2 * fb, s);
+    char* base = (char*)scratch(2 * depth + 1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
     int* ew = error_word(s);
     if (!base || !fbase || !ew) return hipErrorOutOfMemory;
     FT* F = (FT*)(fbase + (phase & 1) * fb);
@@ -1189,8 +1203,15 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         const int a = wf_log2 >= FL ? 0 : (FL - wf_log2 < LK ? FL - wf_log2 : LK);
         const FT* x = F;
         int left = LK - a;
+        bool nest = false;
+        if constexpr (sizeof(KEY) == 4 && MISORT_FENCE_NEST) {
+            static const int nest_min =
+                getenv("MISORT_FENCE_NEST_MIN") ? atoi(getenv("MISORT_FENCE_NEST_MIN")) : 23;
+            nest = depth == 0 && nest_min > 0 && left >= FENCE_NEST_LEVELS && nf >= ((int64_t)1 << nest_min) &&
+                   wf_log2 + a >= KTr<uint64_t>::LW_MIN && wf_log2 + a + left <= KTr<uint64_t>::LWK_MAX;
+        }
         if (a > 0) {
-            FT* y = (left & 1) ? T : M;
+            FT* y = nest || (left & 1) ? T : M;
             const size_t lds = ((size_t)1 << (wf_log2 + a)) * sizeof(FT);
             const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
             // >= 512 blocks where the sub-groups are few (each loads its whole sub-group)
@@ -1205,7 +1226,19 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             }
             x = y;
         }
-        for (int l = a; l < LK; ++l, --left) {
+        if constexpr (sizeof(KEY) == 4) {
+            if (nest) {
+                // the fences' runs of 2^(wf_log2 + a) into M in one pass (it
+                // reads x -- F or T -- and leaves F to k_bounds)
+                const uint64_t* xf = (const uint64_t*)x;
+                const hipError_t e =
+                    left == 4 ? merge_pass<uint64_t, 4>(xf, (uint64_t*)M, nf, wf_log2 + a, s, 0, true, 0, nullptr, false, 1)
+                              : merge_pass<uint64_t, 3>(xf, (uint64_t*)M, nf, wf_log2 + a, s, 0, true, 0, nullptr, false, 1);
+                if (e != hipSuccess) return e;
+                left = 0;
+            }
+        }
+        for (int l = LK - left; l < LK; ++l, --left) {
             FT* y = ((left - 1) & 1) ? T : M;
             const hipError_t e = merge_level<FT>(x, y, nf, wf_log2 + l, s);
             if (e != hipSuccess) return e;
@@ -1280,7 +1313,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     }
     if (hook && !bound) hook->after(KIND_RUNSK_KERNEL, s);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
-    if (probe) {
+    if (probe && depth == 0) {
         // same chunks, outputs to a scratch buffer (the sort is untouched)
         static KEY* junk = nullptr;
         static size_t junk_n = 0;
