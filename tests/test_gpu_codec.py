@@ -1,8 +1,7 @@
-"""The exchange codec (codec.hip) on its own: a sorted run encoded (one pass
-with a decoupled look-back over the blocks' payload counts, or the two-pass
-width / scan / pack form) and decoded must give back the run, and the coded
-size must be the stream format's: 4 header words per 1024-key block plus each
-block's gaps packed at the width of its largest gap.  The reference ships
+"""The exchange codec (codec.hip) on its own: a sorted run encoded (width,
+scans, pack) and decoded must give back the run, and the coded size must be
+the stream format's: 4 header words per 1024-key block plus each block's gaps
+packed at the width of its largest gap.  The reference ships
 uncoded blocks (psort.cc:121-122,146-147); the codec is this framework's own,
 so the expected sizes come from the format, computed here with numpy."""
 import numpy as np
@@ -68,9 +67,8 @@ def test_codec_roundtrip_and_size(ctx, dt, n, kind):
 
 @pytest.mark.parametrize("dt", [np.uint32, np.uint64])
 def test_codec_many_blocks(ctx, dt):
-    """2^24 + 5 keys: 16385 blocks, so every block's look-back walks windows of
-    64 predecessors that are still publishing; repeated encodes reuse the
-    status words (zeroed per launch)."""
+    """2^24 + 5 keys: 16385 blocks, 17 chunks of the payload-offset scan;
+    repeated encodes into the same buffers."""
     n = (1 << 24) + 5
     kt = torch.int32 if dt == np.uint32 else torch.int64
     full = torch.empty(n, dtype=kt, device="cuda")
