@@ -22,6 +22,8 @@
 // scan.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace misort {
@@ -157,52 +159,72 @@ __global__ __launch_bounds__(SCN) void k_scan_chunks(uint32_t* __restrict__ csum
     }
 }
 
-template <typename K>
+// BPW consecutive blocks per workgroup, all their key loads issued before the
+// first block is packed: a block alone is a short chain of dependent steps
+// (loads, LDS, pack, stores), so one per workgroup left the pass latency-bound
+// at eight blocks in flight per CU (MISORT_CODEC_BPW; 1 = one block).
+// Measured (profiles/r05/codec/ab.txt, k = 2^26 u32): encode 0.156 -> 0.141 ms,
+// decode 0.122 -> 0.106 ms with 4; 8 was slower; u64 keys keep one block (the
+// pack equal, the decode's 33 KB of staged payload per workgroup 1.5x slower).
+#ifndef MISORT_CODEC_BPW
+#define MISORT_CODEC_BPW 4
+#endif
+template <typename K, int BPW>
 __global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ kbase, const int64_t* __restrict__ run,
                                                    const uint32_t* __restrict__ off, const uint32_t* __restrict__ coff,
                                                    const uint8_t* __restrict__ wid, uint32_t* __restrict__ out) {
-    __shared__ uint64_t gap[CB];
-    const int64_t b = blockIdx.x, k0 = b * CB;
+    typedef typename std::conditional<sizeof(K) == 4, uint32_t, uint64_t>::type G;  // a gap
+    __shared__ G gap[CB];
+    const int64_t bw = (int64_t)blockIdx.x * BPW;
     const int64_t n = run[1];
-    if (k0 >= n) return;
+    if (bw * CB >= n) return;
     const K* __restrict__ keys = kbase + run[0];
     const int64_t nblk = (n + CB - 1) / CB;
     const int t = threadIdx.x;
-    const int64_t cnt = n - k0 < CB ? n - k0 : CB;
-    {
-        // gap j (key k0+j+1 minus key k0+j) from the lane's run of keys
-        // k0+4t .. k0+4t+3 and the key before it: gap 4t-1+i = x[i+1] - x[i]
-        K x[CI + 1];
-        lane_keys<K>(keys, k0 + (int64_t)t * CI, k0, k0 + cnt, x);
+    // the lane's runs of keys k0+4t .. k0+4t+3 and the key before each, for
+    // every block of the workgroup
+    K x[BPW][CI + 1];
+#pragma unroll
+    for (int u = 0; u < BPW; ++u) {
+        const int64_t k0 = (bw + u) * CB;
+        if (k0 < n) lane_keys<K>(keys, k0 + (int64_t)t * CI, k0, n - k0 < CB ? n : k0 + CB, x[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BPW; ++u) {
+        const int64_t b = bw + u, k0 = b * CB;
+        if (k0 >= n) break;  // uniform
+        const int64_t cnt = n - k0 < CB ? n - k0 : CB;
+        if (u > 0) __syncthreads();  // the previous block's pack has read its gaps
+        // gap j (key k0+j+1 minus key k0+j): gap 4t-1+i = x[i+1] - x[i]
 #pragma unroll
         for (int i = 0; i < CI; ++i) {
             const int j = t * CI + i - 1;
-            if (j >= 0) gap[j] = (j + 1 < cnt) ? (uint64_t)(x[i + 1] - x[i]) : 0;
+            if (j >= 0) gap[j] = (j + 1 < cnt) ? (G)(x[u][i + 1] - x[u][i]) : (G)0;
         }
         if (t == CT - 1) gap[CB - 1] = 0;
-    }
-    __syncthreads();
-    const int w = wid[b];
-    const uint32_t base_w = (uint32_t)(4 * nblk) + off[b] + coff[b / SCN];
-    const int nw = (int)(((cnt - 1) * w + 31) >> 5);
-    if (t == 0) {
-        const uint64_t base = (uint64_t)keys[k0];
-        uint32_t* h = out + 4 * b;
-        h[0] = (uint32_t)base;
-        h[1] = (uint32_t)(base >> 32);
-        h[2] = base_w;
-        h[3] = (uint32_t)w;
-    }
-    for (int q = t; q < nw; q += CT) {
-        // fields j overlapping bits [32q, 32q+32)
-        const int64_t lo = (int64_t)q * 32;
-        uint32_t v = 0;
-        for (int64_t j = lo / w; j * w < lo + 32 && j < cnt - 1; ++j) {
-            const int64_t sh = j * w - lo;  // field start relative to the word (may be < 0)
-            const uint64_t f = gap[j];
-            v |= sh >= 0 ? (uint32_t)(f << sh) : (uint32_t)(f >> (-sh));
+        __syncthreads();
+        const int w = wid[b];
+        const uint32_t base_w = (uint32_t)(4 * nblk) + off[b] + coff[b / SCN];
+        const int nw = (int)(((cnt - 1) * w + 31) >> 5);
+        if (t == 0) {
+            const uint64_t base = (uint64_t)x[u][1];  // lane 0's first key: the block's
+            uint32_t* h = out + 4 * b;
+            h[0] = (uint32_t)base;
+            h[1] = (uint32_t)(base >> 32);
+            h[2] = base_w;
+            h[3] = (uint32_t)w;
         }
-        out[base_w + q] = v;
+        for (int q = t; q < nw; q += CT) {
+            // fields j overlapping bits [32q, 32q+32) (q < 2^11, so 32-bit)
+            const int lo = q * 32;
+            uint32_t v = 0;
+            for (int j = lo / w; j * w < lo + 32 && j < cnt - 1; ++j) {
+                const int sh = j * w - lo;  // field start relative to the word (may be < 0)
+                const uint64_t f = gap[j];
+                v |= sh >= 0 ? (uint32_t)(f << sh) : (uint32_t)(f >> (-sh));
+            }
+            out[base_w + q] = v;
+        }
     }
 }
 
@@ -214,73 +236,92 @@ __global__ void k_set_run(int64_t* run, int64_t offset, int64_t n) {
 // Lane t rebuilds keys 4t..4t+3 of its block: key p = base + the gaps before
 // it, so the lane decodes gaps 4t-1..4t+2, a wave scan (cross-lane shuffles) and one
 // LDS step across the 4 waves give the prefix, and the 4 keys leave as one
-// 16-byte (u32) or two (u64) vector stores.
-template <typename K>
+// 16-byte (u32) or two (u64) vector stores.  BPW blocks per workgroup, as in
+// k_codec_pack: their headers, then their payloads, load at once.
+template <typename K, int BPW>
 __global__ __launch_bounds__(CT) void k_codec_unpack(const uint32_t* __restrict__ in, int64_t n,
                                                      K* __restrict__ keys) {
     static_assert(CI == 4, "one 4-key run per lane");
-    __shared__ uint64_t wsum[CT / 64];
-    // the block's payload words, staged by coalesced loads (each lane's bit
-    // fields then read LDS instead of up to three scattered global words per key)
-    __shared__ uint32_t pay[(CB * 64 + 31) / 32 + 2];
-    const int64_t b = blockIdx.x, k0 = b * CB;
+    constexpr int PW = (CB * 8 * (int)sizeof(K) + 31) / 32 + 2;  // a block's payload words at most, + 2
+    __shared__ uint64_t wsum[BPW][CT / 64];
+    // the blocks' payload words, staged by coalesced loads (each lane's bit
+    // fields then read LDS instead of up to three scattered global words per
+    // key); all BPW blocks' headers, then all their payloads, in flight at once
+    __shared__ uint32_t pay[BPW][PW];
+    const int64_t bw = (int64_t)blockIdx.x * BPW;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int64_t cnt = n - k0 < CB ? n - k0 : CB;
-    const uint32_t* h = in + 4 * b;
-    const uint64_t base = (uint64_t)h[0] | ((uint64_t)h[1] << 32);
-    const uint32_t pw = h[2];
-    const int w = (int)h[3];
-    const uint64_t mask = w >= 64 ? ~0ull : ((1ull << w) - 1);
-    const int nw = (int)(((cnt - 1) * w + 31) >> 5);
-    for (int q = t; q < nw; q += CT) pay[q] = in[pw + q];
-    if (t < 2) pay[nw + t] = 0u;  // a field's read of the words past the payload
-    __syncthreads();
-    uint64_t g[CI], s = 0;
+    uint64_t base[BPW];
+    uint32_t pw[BPW];
+    int w[BPW], nw[BPW];
+    int64_t cnt[BPW];
 #pragma unroll
-    for (int i = 0; i < CI; ++i) {
-        const int64_t j = (int64_t)t * CI + i - 1;  // the gap before key 4t+i
-        uint64_t f = 0;
-        if (w && j >= 0 && j + 1 < cnt) {
-            const int64_t bit = j * w;
-            const uint32_t* p = pay + (bit >> 5);
-            const int sh = (int)(bit & 31);
-            const uint64_t lo = (uint64_t)p[0] | ((uint64_t)(sh + w > 32 ? p[1] : 0) << 32);
-            f = lo >> sh;
-            if (sh + w > 64) f |= (uint64_t)p[2] << (64 - sh);
-            f &= mask;
+    for (int u = 0; u < BPW; ++u) {
+        const int64_t k0 = (bw + u) * CB;
+        cnt[u] = k0 >= n ? 0 : (n - k0 < CB ? n - k0 : CB);
+        const uint32_t* h = in + 4 * (bw + u);
+        base[u] = cnt[u] ? (uint64_t)h[0] | ((uint64_t)h[1] << 32) : 0;
+        pw[u] = cnt[u] ? h[2] : 0;
+        w[u] = cnt[u] ? (int)h[3] : 0;
+        nw[u] = cnt[u] ? (int)(((cnt[u] - 1) * w[u] + 31) >> 5) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < BPW; ++u) {
+        for (int q = t; q < nw[u]; q += CT) pay[u][q] = in[pw[u] + q];
+        if (t < 2) pay[u][nw[u] + t] = 0u;  // a field's read of the words past the payload
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < BPW; ++u) {
+        if (cnt[u] == 0) break;  // uniform
+        const int64_t k0 = (bw + u) * CB;
+        const uint64_t mask = w[u] >= 64 ? ~0ull : ((1ull << w[u]) - 1);
+        uint64_t g[CI], s = 0;
+#pragma unroll
+        for (int i = 0; i < CI; ++i) {
+            const int j = t * CI + i - 1;  // the gap before key 4t+i
+            uint64_t f = 0;
+            if (w[u] && j >= 0 && j + 1 < cnt[u]) {
+                const int bit = j * w[u];
+                const uint32_t* p = pay[u] + (bit >> 5);
+                const int sh = bit & 31;
+                const uint64_t lo = (uint64_t)p[0] | ((uint64_t)(sh + w[u] > 32 ? p[1] : 0) << 32);
+                f = lo >> sh;
+                if (sh + w[u] > 64) f |= (uint64_t)p[2] << (64 - sh);
+                f &= mask;
+            }
+            s += f;
+            g[i] = s;  // inclusive prefix within the lane
         }
-        s += f;
-        g[i] = s;  // inclusive prefix within the lane
-    }
-    uint64_t x = s;  // inclusive scan of the lane totals over the wave
+        uint64_t x = s;  // inclusive scan of the lane totals over the wave
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint64_t pre = x - s;
-    for (int v = 0; v < wv; ++v) pre += wsum[v];
-    K r[CI];
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[u][wv] = x;
+        __syncthreads();
+        uint64_t pre = x - s;
+        for (int v = 0; v < wv; ++v) pre += wsum[u][v];
+        K r[CI];
 #pragma unroll
-    for (int i = 0; i < CI; ++i) r[i] = (K)(base + pre + g[i]);
-    const int64_t p0 = k0 + (int64_t)t * CI;
-    if ((int64_t)t * CI + CI <= cnt && !((uintptr_t)(keys + p0) & 15)) {
-        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-        v4* dst = reinterpret_cast<v4*>(keys + p0);
-        if constexpr (sizeof(K) == 4) {
-            dst[0] = v4{(uint32_t)r[0], (uint32_t)r[1], (uint32_t)r[2], (uint32_t)r[3]};
+        for (int i = 0; i < CI; ++i) r[i] = (K)(base[u] + pre + g[i]);
+        const int64_t p0 = k0 + (int64_t)t * CI;
+        if ((int64_t)t * CI + CI <= cnt[u] && !((uintptr_t)(keys + p0) & 15)) {
+            typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+            v4* dst = reinterpret_cast<v4*>(keys + p0);
+            if constexpr (sizeof(K) == 4) {
+                dst[0] = v4{(uint32_t)r[0], (uint32_t)r[1], (uint32_t)r[2], (uint32_t)r[3]};
+            } else {
+                dst[0] = v4{(uint32_t)r[0], (uint32_t)((uint64_t)r[0] >> 32), (uint32_t)r[1],
+                            (uint32_t)((uint64_t)r[1] >> 32)};
+                dst[1] = v4{(uint32_t)r[2], (uint32_t)((uint64_t)r[2] >> 32), (uint32_t)r[3],
+                            (uint32_t)((uint64_t)r[3] >> 32)};
+            }
         } else {
-            dst[0] = v4{(uint32_t)r[0], (uint32_t)((uint64_t)r[0] >> 32), (uint32_t)r[1],
-                        (uint32_t)((uint64_t)r[1] >> 32)};
-            dst[1] = v4{(uint32_t)r[2], (uint32_t)((uint64_t)r[2] >> 32), (uint32_t)r[3],
-                        (uint32_t)((uint64_t)r[3] >> 32)};
-        }
-    } else {
 #pragma unroll
-        for (int i = 0; i < CI; ++i)
-            if ((int64_t)t * CI + i < cnt) keys[p0 + i] = r[i];
+            for (int i = 0; i < CI; ++i)
+                if ((int64_t)t * CI + i < cnt[u]) keys[p0 + i] = r[i];
+        }
     }
 }
 
@@ -315,7 +356,8 @@ hipError_t codec_encode_dev(const K* base, const int64_t* run, int64_t n_max, ui
     k_codec_width<K><<<(unsigned)nb, CT, 0, s>>>(base, run, words, wid);
     k_scan_words<<<(unsigned)nc, SCN, 0, s>>>(words, nb, off, csum);
     k_scan_chunks<<<1, SCN, 0, s>>>(csum, nc, run, (int)(sizeof(K) / 4), sizes);
-    k_codec_pack<K><<<(unsigned)nb, CT, 0, s>>>(base, run, off, csum, wid, out);
+    constexpr int BPW = sizeof(K) == 4 ? MISORT_CODEC_BPW : 1;  // u64: equal (pack) / slower (unpack)
+    k_codec_pack<K, BPW><<<(unsigned)((nb + BPW - 1) / BPW), CT, 0, s>>>(base, run, off, csum, wid, out);
     return hipGetLastError();
 }
 
@@ -332,7 +374,8 @@ hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, 
 template <typename K>
 hipError_t codec_decode(const uint32_t* in, int64_t n, K* keys, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    k_codec_unpack<K><<<(unsigned)codec_blocks(n), CT, 0, s>>>(in, n, keys);
+    constexpr int BPW = sizeof(K) == 4 ? MISORT_CODEC_BPW : 1;  // u64: 33 KB of payload LDS per workgroup
+    k_codec_unpack<K, BPW><<<(unsigned)((codec_blocks(n) + BPW - 1) / BPW), CT, 0, s>>>(in, n, keys);
     return hipGetLastError();
 }
 

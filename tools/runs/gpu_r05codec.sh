@@ -1,15 +1,13 @@
-# codec A/B: tests under the default (one-pass encoder, one-wave blocks) and the
-# 256-lane fused form, then encode/decode times of three builds, then the
-# multi-rank and RCCL tests under the default.
+# codec A/B: tests under the default build, then encode/decode times of
+# $VARIANTS builds (lib/variants, base = lib), then the multi-rank and RCCL
+# tests under the default.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; O="$R/gpurun_out/codec"; mkdir -p "$O"; cd "$R"
 V="$R/parallel-computing-mpi_amd/lib/variants"
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_codec.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/pytest_codec.log" 2>&1 || { tail -30 "$O/pytest_codec.log"; exit 1; }
 tail -1 "$O/pytest_codec.log"
-MISORT_LIBRARY=$V/libmisort_f256.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_codec.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/pytest_codec_f256.log" 2>&1 || { tail -30 "$O/pytest_codec_f256.log"; exit 1; }
-tail -1 "$O/pytest_codec_f256.log"
 for rep in 1 2; do
-  for v in fused0 f256 base; do
+  for v in ${VARIANTS:-bpw1 bpw8 base}; do
     if [ $v = base ]; then unset MISORT_LIBRARY; else export MISORT_LIBRARY=$V/libmisort_$v.so; fi
     timeout -k 10 120 python3 -u tools/codec_probe.py > "$O/${v}_$rep.jsonl" || exit 1
     python3 -c "
