@@ -127,6 +127,14 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_WGCU16
 #define MISORT_MK_WGCU16 3
 #endif
+// 16-way passes: keys per load row (a row lies in one segment; the chunk
+// descriptor holds 8 bytes per row).  128 instead of 64 halves the
+// descriptors (1664 -> 896 bytes per chunk): 2^30 u32 pass 2569 -> 2547 us,
+// 2^26 -1.8 %, u64 2^29 -9 us per pass, k_mergek itself equal
+// (profiles/r05/plan/rw_ab.txt).
+#ifndef MISORT_MK_RW16
+#define MISORT_MK_RW16 128
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -207,7 +215,7 @@ struct Shape {
     __device__ __host__ static int seg(int o, int q) { return CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G; }
     static constexpr int K = 1 << LK, LKS = LK;
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
-    static constexpr int RW = LK == 4 ? 64 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
+    static constexpr int RW = LK == 4 ? MISORT_MK_RW16 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
     // load slots per lane: enough rows for CAP keys in K segments (18 at
     // CAP = 8192, IT = 17 or 18)
