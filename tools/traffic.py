@@ -20,9 +20,9 @@ guide's 16-B rule, as before round 4.
 The merge levels (runs.hip) are two launches per level: run_merge =
 k_runs_merge + k_runs_partition per level.  The multi-way merge pass (runsk.hip)
 is k_mergek plus its small planning kernels (k_fence_gather on the first
-multi-way pass, k_fence_merge / k_fence_lds or the u64 fence merge levels,
-k_fence_counts, k_scan_totals, k_bounds, k_chunk_desc); "run_mergek" sums them
-per launch of k_mergek.
+multi-way pass, k_fence_merge / k_fence_lds or the u64 fence merge levels or
+the nested u64 multi-way pass over the fences, k_fence_counts, k_scan_totals,
+k_bounds, k_chunk_desc); "run_mergek" sums them per launch of k_mergek.
     WORKLOAD=u32_2e30_n1 tools/traffic.py gpurun_out/pmc30 > profiles/traffic.json
 ("workload" must match bench.py's f"{dtype}_2e{logn}_n{ranks}" for bench to use it).
 """
@@ -87,7 +87,9 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
         elif "k_runs_partition" in name:
             fam = "run_partition"
         elif "k_mergek" in name:
-            fam = "run_mergek_kernel"
+            # u32 sorts: k_mergek on unsigned long is a pass's nested fence
+            # merge (runsk.hip MISORT_FENCE_NEST), planning of that pass
+            fam = "runk_plan" if U32 and "k_mergek<unsigned long" in name else "run_mergek_kernel"
         elif re.search(r"k_fence_gather|k_fence_lds|k_fence_merge|k_fence_counts|k_scan_totals|k_bounds|k_chunk_desc",
                        name):
             fam = "runk_plan"
