@@ -438,6 +438,11 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 #ifndef MISORT_FC_U32
 #define MISORT_FC_U32 1
 #endif
+// the coalesced form's fences per lane in flight (their loads issued together;
+// 2^30 pass -7 us, u64 2^29 -10 us, profiles/r05/plan/fcb_ab.txt)
+#ifndef MISORT_FC_BATCH
+#define MISORT_FC_BATCH 8
+#endif
 constexpr int COUNT_NT = 1024;
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
@@ -506,13 +511,26 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
         }
         if (cur >= 0) flush(cur, lo8, hi8);
     } else if (tid < SCAN_NT) {
-        for (int64_t e = f0 + tid; e < f1; e += SCAN_NT) {
-            const int r = (int)((ftag(M[e]) >> (32 - geo.lk)) & (K - 1));
+        // FCB fences per lane in flight: their loads first, then their counts
+        constexpr int FCB = MISORT_FC_BATCH;
+        for (int64_t e0 = f0 + tid; e0 < f1; e0 += FCB * SCAN_NT) {
+            uint32_t tg[FCB];
+#pragma unroll
+            for (int u = 0; u < FCB; ++u) {
+                const int64_t e = e0 + (int64_t)u * SCAN_NT;
+                tg[u] = e < f1 ? ftag(M[e]) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < FCB; ++u) {
+                const int64_t e = e0 + (int64_t)u * SCAN_NT;
+                if (e >= f1) break;
+                const int r = (int)((tg[u] >> (32 - geo.lk)) & (K - 1));
 #if MISORT_FC_U32
-            atomicAdd(&sc[chunk_of(e)][r], 1u);
+                atomicAdd(&sc[chunk_of(e)][r], 1u);
 #else
-            atomicAdd(&sc[chunk_of(e)][r >> 3], 1ull << (8 * (r & 7)));
+                atomicAdd(&sc[chunk_of(e)][r >> 3], 1ull << (8 * (r & 7)));
 #endif
+            }
         }
     }
     __syncthreads();
