@@ -166,13 +166,16 @@ static_assert(KTr<uint32_t>::NT == 256 || KTr<uint32_t>::NT == 384 || KTr<uint32
 #ifndef MISORT_MK_CAP64
 #define MISORT_MK_CAP64 8832
 #endif
+#ifndef MISORT_MK_WGCU64
+#define MISORT_MK_WGCU64 2
+#endif
 template <>
 struct KTr<uint64_t> {
     typedef u128 F;
     static constexpr int NT = 512;
     static constexpr int IT = MISORT_MK_IT64;
     static constexpr int CAP = MISORT_MK_CAP64;  // 69 KiB of keys: two tiles per CU, 4 waves per SIMD
-    static constexpr int WG_PER_CU = 2;
+    static constexpr int WG_PER_CU = MISORT_MK_WGCU64;
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
     static constexpr int it(int) { return IT; }
