@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--dtype", choices=["u32", "u64"], default="u64")
 ap.add_argument("--logn", type=int, default=29)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--hi", type=int, default=0, help="13: the u32 2^14 merge-level tile (default: the largest tile)")
 a = ap.parse_args()
 n = 1 << a.logn
 T = (torch.uint32 if hasattr(torch, "uint32") else torch.int32) if a.dtype == "u32" else \
@@ -25,7 +26,7 @@ ctx = misort.Context(0)
 d = torch.empty(n, dtype=T, device="cuda")
 ctx.fill_splitmix(d, 0x5EED0003)
 o = torch.empty_like(d)
-ms = ctx.pass_probe(d, o, "tile_sort", 0, 0, False, reps=a.reps)
-print(json.dumps({"dtype": a.dtype, "logn": a.logn, "sort_pass_ms": ms,
+ms = ctx.pass_probe(d, o, "tile_sort", a.hi, 0, False, reps=a.reps)
+print(json.dumps({"dtype": a.dtype, "logn": a.logn, "hi": a.hi, "sort_pass_ms": ms,
                   "library": os.path.basename(misort.library_path())}))
 ctx.close()
