@@ -597,6 +597,11 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #ifndef MISORT_SORT_PT
 #define MISORT_SORT_PT 0
 #endif
+// the merge levels' pair of a lane by its position over the level's constant
+// pair stride (all the tile's runs have one length)
+#ifndef MISORT_SORT_UNIGEO
+#define MISORT_SORT_UNIGEO 1
+#endif
 template <typename KEY, int LT, int F>
 struct SortMergeShape {
     static_assert(F >= 7 && F <= 12 && F <= LT, "merge levels from runs of 64 .. 2^11 keys");
@@ -626,6 +631,10 @@ struct SortMergeShape {
     // table sits past the level layouts, 16-byte aligned
     static constexpr bool ZW = MISORT_SORT_ZW && CH == 1;
     static constexpr bool PT = MISORT_SORT_PT && K > 2;
+    // uniform geometry: K runs of RUN keys at a stride of RUN + GS (lds_merge.h
+    // shape_uni); u32 tile 3346 -> 3314 us at 2^30, u64 +14 us (kept off),
+    // profiles/r05/tile/unigeo_ab.txt
+    static constexpr bool UNI = MISORT_SORT_UNIGEO && !PT && sizeof(KEY) == 4;
     static constexpr int PT_AT = (WORDS + 3) & ~3;
     static constexpr int PT_WORDS = PT ? (K / 2) * (int)(sizeof(PairRec) / sizeof(KEY)) : 0;
     static constexpr int ALL_WORDS = PT ? PT_AT + PT_WORDS : WORDS;

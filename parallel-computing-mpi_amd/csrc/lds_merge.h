@@ -314,6 +314,28 @@ template <typename S>
 struct shape_pt<S, decltype((void)S::PT)> {
     static constexpr bool v = S::PT;
 };
+// UNI (the SORT tile's merge levels): all K sequences are S::RUN keys long and
+// sequence q starts at q * (S::RUN + S::GS), so every level's pairs sit at a
+// constant stride and a lane's pair is its position over that stride -- in
+// place of per-pair selects on constants (a v_mov and a v_cndmask each).
+template <typename S, typename = void>
+struct shape_uni {
+    static constexpr bool v = false;
+};
+template <typename S>
+struct shape_uni<S, decltype((void)S::UNI)> {
+    static constexpr bool v = S::UNI;
+};
+// A uniform shape's level lv: its input sequences' length and stride and its
+// pairs' stride (level_geometry's rounding of each output + G up to QA).
+template <typename S>
+constexpr int uni_len(int lv) { return S::RUN << (lv - 1); }
+template <typename S>
+constexpr int uni_stride(int lv) {  // the stride of level lv's outputs (lv >= 1)
+    return (2 * uni_len<S>(lv) + S::G + S::QA - 1) / S::QA * S::QA;
+}
+template <typename S>
+constexpr int uni_in_stride(int lv) { return lv == 1 ? S::RUN + S::GS : uni_stride<S>(lv - 1); }
 
 // Pair p of a level as the lanes read it from the pair table: A and B
 // (start, length), the output start and length; 8 ints per pair.
@@ -413,7 +435,17 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
         // the lane's pair: the last one starting at or before pos
         int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
         if (P > 1) {
-            if constexpr (shape_pt<S>::v) {
+            if constexpr (shape_uni<S>::v) {
+                const int SL = uni_stride<S>(lv), SI = uni_in_stride<S>(lv), L0 = uni_len<S>(lv);
+                int pi = pos / SL;
+                pi = pi < P - 1 ? pi : P - 1;
+                A0 = 2 * pi * SI;
+                LA = L0;
+                B0 = A0 + SI;
+                LB = L0;
+                Q = pi * SL;
+                LP = 2 * L0;
+            } else if constexpr (shape_pt<S>::v) {
                 int pi = 0;
 #pragma unroll
                 for (int p = 1; p < K / 2; ++p)
