@@ -79,6 +79,11 @@ struct KTr;
 #ifndef MISORT_FENCE_MERGE
 #define MISORT_FENCE_MERGE 1
 #endif
+// bytes of the aligned window k_bounds reads around its interpolated guess
+// (64: u32 passes -1..-10 us, u64 +2 us, profiles/r05/plan/bl64_ab.txt -- noise level)
+#ifndef MISORT_BOUNDS_LINE
+#define MISORT_BOUNDS_LINE 128
+#endif
 constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 // u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
 // VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
@@ -671,7 +676,7 @@ __device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<K
     // before it); otherwise it narrows the range to one side.  It cuts the
     // dependent probe rounds, which pays when many searches share the memory
     // system; a few thousand latency-bound ones run faster without it.
-    constexpr int BW = 128 / (int)sizeof(KEY);
+    constexpr int BW = MISORT_BOUNDS_LINE / (int)sizeof(KEY);
     const int64_t blk = (p < b ? p : b - 1) & ~(int64_t)(BW - 1);
     bool fwd;
     if (line && a < b && blk + BW <= len && ((uintptr_t)kr & 15) == 0) {
