@@ -95,6 +95,10 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_ZW
 #define MISORT_MK_ZW 1
 #endif
+// zero words for the one-key chain too (the u64 passes; one more sentinel word)
+#ifndef MISORT_MK_ZW_CH0
+#define MISORT_MK_ZW_CH0 0
+#endif
 
 #ifndef MISORT_MK_PT
 #define MISORT_MK_PT 0
@@ -212,7 +216,7 @@ struct Shape {
     // MISORT_MK_ZW): the last of the G words after a sequence holds the next
     // one's, so G exceeds the keys a chain reads past a sequence (IT for the
     // two-key chains, IT + 1 for the one-key chain)
-    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2);
+    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2 || (CH == 0 && MISORT_MK_ZW_CH0));
     static constexpr int G = CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
     // level outputs start at lane boundaries; chain 3 also needs even slots
     static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
