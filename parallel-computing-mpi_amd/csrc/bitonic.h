@@ -540,15 +540,15 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 #pragma unroll
         for (int j = 0; j < G::V; ++j) x[j] = s[pad(e + j)];
         store_slot<K, LT>(out, tile, n, full, e, x);
-        constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
+        // flk = the first pass's lk | its fence stride (log2) << 8 (0: MERGEK_FENCE_LOG2)
+        const int fgl = (flk >> 8) ? (flk >> 8) : MERGEK_FENCE_LOG2, lkf = flk & 0xFF;
         const int64_t gi = (tile << LT) + e;
-        if (fence && (e & FGM) == 0 && gi < n) {
-            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
-                                 (uint32_t)(e >> MERGEK_FENCE_LOG2);
+        if (fence && (e & ((1 << fgl) - 1)) == 0 && gi < n) {
+            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << lkf) - 1)) << (32 - lkf)) | (uint32_t)(e >> fgl);
             if constexpr (sizeof(K) == 4)
-                ((uint64_t*)fence)[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
+                ((uint64_t*)fence)[gi >> fgl] = ((uint64_t)x[0] << 32) | tag;
             else
-                ((unsigned __int128*)fence)[gi >> MERGEK_FENCE_LOG2] = ((unsigned __int128)x[0] << 64) | tag;
+                ((unsigned __int128*)fence)[gi >> fgl] = ((unsigned __int128)x[0] << 64) | tag;
         }
     }
 }
@@ -702,15 +702,15 @@ __device__ __forceinline__ void final_store_plain(const K* s, K* out, int64_t ti
 #pragma unroll
         for (int j = 0; j < G::V; ++j) x[j] = v[j];
         store_slot<K, LT>(out, tile, n, full, e, x);
-        constexpr int FGM = (1 << MERGEK_FENCE_LOG2) - 1;
+        // flk = the first pass's lk | its fence stride (log2) << 8 (0: MERGEK_FENCE_LOG2)
+        const int fgl = (flk >> 8) ? (flk >> 8) : MERGEK_FENCE_LOG2, lkf = flk & 0xFF;
         const int64_t gi = (tile << LT) + e;
-        if (fence && (e & FGM) == 0 && gi < n) {
-            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << flk) - 1)) << (32 - flk)) |
-                                 (uint32_t)(e >> MERGEK_FENCE_LOG2);
+        if (fence && (e & ((1 << fgl) - 1)) == 0 && gi < n) {
+            const uint32_t tag = ((uint32_t)((gi >> LT) & ((1 << lkf) - 1)) << (32 - lkf)) | (uint32_t)(e >> fgl);
             if constexpr (sizeof(K) == 4)
-                ((uint64_t*)fence)[gi >> MERGEK_FENCE_LOG2] = ((uint64_t)x[0] << 32) | tag;
+                ((uint64_t*)fence)[gi >> fgl] = ((uint64_t)x[0] << 32) | tag;
             else
-                ((unsigned __int128*)fence)[gi >> MERGEK_FENCE_LOG2] = ((unsigned __int128)x[0] << 64) | tag;
+                ((unsigned __int128*)fence)[gi >> fgl] = ((unsigned __int128)x[0] << 64) | tag;
         }
     }
 }
@@ -1068,6 +1068,9 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
     const double bytes = 2.0 * (double)n * sizeof(K);
     const K* src = in;
     int fence_phase = 0;  // multi-way passes: fence buffer holding the next pass's fences
+    // the multi-way passes' fence stride: 64-key fences (runsk_fg6.hip) for
+    // large sorts, every pass of one sort the same build
+    const bool fg6 = mergek_fence_log2(n, (int)sizeof(K)) == 6;
     // the SORT pass writes the first multi-way pass's fences (no gather pass)
     // unless it runs chunk by chunk (host staging)
     const bool sort_fences = np > 1 && ps[1].kind == KIND_RUNSK && ps[1].hi == LT && !(io && io->before_first);
@@ -1091,10 +1094,12 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
             if constexpr (sizeof(K) == 8) {
                 // the last pass stores IEEE double bits itself
                 const bool oo = ord_out && i == np - 1;
-                e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh, oo);
+                e = fg6 ? merge_levelk_fg6(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh, oo)
+                        : merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh, oo);
                 if (oo && e == hipSuccess) ord_out = false;
             } else {
-                e = merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh);
+                e = fg6 ? merge_levelk_fg6(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh)
+                        : merge_levelk(src, dst, n, p.hi, p.R, s, fence_phase, !prevk, lk_next, kh);
             }
             if (e != hipSuccess) return e;
             fence_phase ^= 1;
@@ -1127,10 +1132,11 @@ hipError_t local_sort_impl(const K* in, K* out, int64_t n, bool ord_in, K* scrat
             if (bind) (void)hook->bind(KIND_TILE_SORT, -1, bytes, &ea, &eb);
             void* f = nullptr;
             if (i == 0 && sort_fences) {
-                f = mergek_fence_buffer(n, (int)sizeof(K), 0, s);
+                f = fg6 ? mergek_fence_buffer_fg6(n, (int)sizeof(K), 0, s) : mergek_fence_buffer(n, (int)sizeof(K), 0, s);
                 if (!f) return hipErrorOutOfMemory;
             }
-            launch_sort<K>(src, dst, n, ord_in, s, LT, f, f ? ps[1].R : 0, ea, eb);
+            // flk: the first pass's lk and, above bit 8, the fence stride
+            launch_sort<K>(src, dst, n, ord_in, s, LT, f, f ? ps[1].R | ((fg6 ? 6 : MERGEK_FENCE_LOG2) << 8) : 0, ea, eb);
         }
         src = dst;
     }

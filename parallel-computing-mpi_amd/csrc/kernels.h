@@ -171,6 +171,18 @@ constexpr int SORT_LT_U32 = 15, SORT_LT_MERGE = 14;
 void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s);
 void mergek_release(hipStream_t s);
 int mergek_take_error(hipStream_t s);
+// The same entry points of the 64-key-fence build (runsk_fg6.hip).
+hipError_t merge_levelk_fg6(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                            bool gather, int lk_next, LaunchHook* hook = nullptr);
+hipError_t merge_levelk_fg6(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+                            bool gather, int lk_next, LaunchHook* hook = nullptr, bool ord_out = false);
+int64_t mergek_chunks_fg6(int64_t n, int lw, int lk, int key_bytes);
+void* mergek_fence_buffer_fg6(int64_t n, int key_bytes, int phase, hipStream_t s);
+void mergek_release_fg6(hipStream_t s);
+int mergek_take_error_fg6(hipStream_t s);
+// The fence stride (log2 keys) the local sort of n keys uses: 6 (runsk_fg6)
+// from 2^MISORT_FENCE_FG6_MIN keys (u32: 30, u64: 29), else MERGEK_FENCE_LOG2.
+int mergek_fence_log2(int64_t n, int key_bytes);
 int merge_levelk_lw_min(int key_bytes);   // shortest input runs (log2) of a multi-way pass
 int merge_levelk_lwk_max(int key_bytes);  // largest output runs (log2)
 

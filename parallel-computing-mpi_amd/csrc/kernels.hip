@@ -32,6 +32,16 @@ const PlanKnobs& plan_knobs() {
     return k;
 }
 
+int mergek_fence_log2(int64_t n, int key_bytes) {
+    // MISORT_FENCE_FG6_MIN (u32) / MISORT_FENCE_FG6_MIN_U64: log2 keys from which
+    // the 64-key fences pay (fuller chunks against twice the fences to merge,
+    // count and search; profiles/r05/plan/fg6_ab.txt); 0 = never
+    static const int m32 = getenv("MISORT_FENCE_FG6_MIN") ? atoi(getenv("MISORT_FENCE_FG6_MIN")) : 30;
+    static const int m64 = getenv("MISORT_FENCE_FG6_MIN_U64") ? atoi(getenv("MISORT_FENCE_FG6_MIN_U64")) : 29;
+    const int m = key_bytes == 8 ? m64 : m32;
+    return m > 0 && m < 63 && n >= ((int64_t)1 << m) ? 6 : MERGEK_FENCE_LOG2;
+}
+
 // The largest SORT tile per key type (log2 keys): every plan's tiles divide it.
 int tile_log2(int key_bytes) { return key_bytes == 4 ? KT<uint32_t>::LT : KT<uint64_t>::LT; }
 

@@ -46,7 +46,16 @@
 namespace misort {
 namespace {
 
-constexpr int FG_LOG2 = MERGEK_FENCE_LOG2;  // kernels.h (the u32 SORT pass writes fences too)
+// The fence stride: MERGEK_FENCE_LOG2 (kernels.h), or MISORT_RUNSK_FGL in the
+// second build of this file (runsk_fg6.hip: 64-key fences, its entry points
+// suffixed by MISORT_RUNSK_FN).
+#ifndef MISORT_RUNSK_FGL
+#define MISORT_RUNSK_FGL MERGEK_FENCE_LOG2
+#endif
+#ifndef MISORT_RUNSK_FN
+#define MISORT_RUNSK_FN(x) x
+#endif
+constexpr int FG_LOG2 = MISORT_RUNSK_FGL;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
 #ifndef MISORT_MK_NT
 #define MISORT_MK_NT 512
@@ -1385,7 +1394,7 @@ hipError_t merge_levelk_t(const KEY* src, KEY* dst, int64_t n, int lw, int lk, h
 
 }  // namespace
 
-int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes) {
+int64_t MISORT_RUNSK_FN(mergek_chunks)(int64_t n, int lw, int lk, int key_bytes) {
     return key_bytes == 8 ? chunks_of(make_geo<uint64_t>(n, lw, lk)) : chunks_of(make_geo<uint32_t>(n, lw, lk));
 }
 
@@ -1393,15 +1402,15 @@ int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes) {
 // (gather: build them from src first); lk_next > 0: write the next multi-way
 // pass's fences (runs of 2^(lw+lk) in groups of 2^lk_next) into the other
 // buffer.
-hipError_t merge_levelk(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+hipError_t MISORT_RUNSK_FN(merge_levelk)(const uint32_t* src, uint32_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next, LaunchHook* hook) {
     return merge_levelk_t<uint32_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook);
 }
-hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
+hipError_t MISORT_RUNSK_FN(merge_levelk)(const uint64_t* src, uint64_t* dst, int64_t n, int lw, int lk, hipStream_t s, int phase,
                         bool gather, int lk_next, LaunchHook* hook, bool ord_out) {
     return merge_levelk_t<uint64_t>(src, dst, n, lw, lk, s, phase, gather, lk_next, hook, ord_out);
 }
-void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
+void* MISORT_RUNSK_FN(mergek_fence_buffer)(int64_t n, int key_bytes, int phase, hipStream_t s) {
     // the sizes merge_pass computes, so the buffer never moves between the two
     const int64_t nf = (n + FG - 1) >> FG_LOG2;
     const size_t fb = ((size_t)nf * (key_bytes == 8 ? sizeof(u128) : sizeof(uint64_t)) + 255) & ~(size_t)255;
@@ -1410,7 +1419,7 @@ void* mergek_fence_buffer(int64_t n, int key_bytes, int phase, hipStream_t s) {
 }
 // 1 if a merge pass on stream s rejected a chunk since the last call (the
 // stream is synchronised), else 0; negative on a HIP error.
-int mergek_take_error(hipStream_t s) {
+int MISORT_RUNSK_FN(mergek_take_error)(hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     int* w = nullptr;
@@ -1430,7 +1439,7 @@ int mergek_take_error(hipStream_t s) {
 
 // Frees the fence and planning scratch kept for stream s on the current
 // device (misort_destroy, for the context's own stream).
-void mergek_release(hipStream_t s) {
+void MISORT_RUNSK_FN(mergek_release)(hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return;
     std::lock_guard<std::mutex> g(g_mu);
@@ -1450,7 +1459,9 @@ void mergek_release(hipStream_t s) {
         m.erase(it);
     }
 }
+#ifndef MISORT_RUNSK_SECOND
 int merge_levelk_lw_min(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LW_MIN : KTr<uint32_t>::LW_MIN; }
 int merge_levelk_lwk_max(int key_bytes) { return key_bytes == 8 ? KTr<uint64_t>::LWK_MAX : KTr<uint32_t>::LWK_MAX; }
+#endif
 
 }  // namespace misort

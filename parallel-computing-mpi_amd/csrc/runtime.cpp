@@ -845,7 +845,8 @@ int fetch(misort_ctx* c, hipStream_t s, std::initializer_list<D2H> cps) {
 // The merge passes' device error word of stream s (k_chunk_desc rejected a
 // chunk): the stream is synchronised.
 int planning_check(hipStream_t s) {
-    const int e = misort::mergek_take_error(s);
+    const int e0 = misort::mergek_take_error(s), e1 = misort::mergek_take_error_fg6(s);
+    const int e = e0 < 0 || e1 < 0 ? -1 : (e0 | e1);
     if (e < 0) return fail(MISORT_E_HIP, "reading the merge passes' error word failed");
     if (e > 0) return fail(MISORT_E_INTERNAL, "a merge pass rejected its chunk bounds: the sorted output is incomplete");
     return MISORT_OK;
@@ -1642,6 +1643,7 @@ int misort_destroy(misort_ctx* c) {
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->stream) {
         misort::mergek_release(c->stream);  // the merge passes' scratch for this stream
+        misort::mergek_release_fg6(c->stream);
         (void)hipStreamDestroy(c->stream);
     }
     delete c;

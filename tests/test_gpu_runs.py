@@ -221,6 +221,13 @@ ctx.close()
     (4, {"MISORT_FENCE_NEST_MIN": "12"}, (1 << 27) + 777),
     (4, {"MISORT_FENCE_NEST_MIN": "12", "MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),
     (4, {"MISORT_FENCE_NEST_MIN": "0"}, (1 << 27) + 777),  # never nested
+    # 64-key fences (runsk_fg6.hip; the default from 2^30 u32 / 2^29 u64 keys)
+    (4, {"MISORT_FENCE_FG6_MIN": "20"}, (1 << 26) + 12345),
+    (4, {"MISORT_FENCE_FG6_MIN": "20"}, (1 << 27) + 777),
+    (4, {"MISORT_FENCE_FG6_MIN": "20", "MISORT_FENCE_NEST_MIN": "12"}, (1 << 26) + 12345),
+    (4, {"MISORT_FENCE_FG6_MIN": "20", "MISORT_MULTIWAY": "3"}, (1 << 24) + 12345),
+    (8, {"MISORT_FENCE_FG6_MIN_U64": "20"}, (1 << 25) + 12345),
+    (8, {"MISORT_FENCE_FG6_MIN_U64": "20"}, (1 << 22) + 3),
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
     (8, {"MISORT_RUN_NT": "512"}, (1 << 20) + 5),
