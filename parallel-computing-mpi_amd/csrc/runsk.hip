@@ -464,7 +464,16 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 #ifndef MISORT_FC_BATCH
 #define MISORT_FC_BATCH 8
 #endif
-constexpr int COUNT_NT = 1024;
+// lanes of the coalesced form's block (it counts with all of them; the scan
+// uses the first SCAN_NT): 512 instead of 256 measured 2^30 pass -6 us, u64
+// 2^29 -5 us, 2^28 equal (profiles/r05/plan/fcnt_ab.txt).  Reading the whole
+// fence window in k_bounds instead of its interpolated line measured slower at
+// every size (2^30 pass +36 us; profiles/r05/plan/win_ab.txt).
+#ifndef MISORT_FC_NT
+#define MISORT_FC_NT 512
+#endif
+constexpr int COUNT_NT = 1024, FC_NT = MISORT_FC_NT;
+static_assert(FC_NT >= SCAN_NT && FC_NT <= COUNT_NT && FC_NT % 64 == 0, "fence-count block");
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
                                                            int cpb, int* __restrict__ P, int* __restrict__ bsum) {
@@ -531,19 +540,19 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
             else hi8 += one;
         }
         if (cur >= 0) flush(cur, lo8, hi8);
-    } else if (tid < SCAN_NT) {
+    } else {
         // FCB fences per lane in flight: their loads first, then their counts
         constexpr int FCB = MISORT_FC_BATCH;
-        for (int64_t e0 = f0 + tid; e0 < f1; e0 += FCB * SCAN_NT) {
+        for (int64_t e0 = f0 + tid; e0 < f1; e0 += FCB * FC_NT) {
             uint32_t tg[FCB];
 #pragma unroll
             for (int u = 0; u < FCB; ++u) {
-                const int64_t e = e0 + (int64_t)u * SCAN_NT;
+                const int64_t e = e0 + (int64_t)u * FC_NT;
                 tg[u] = e < f1 ? ftag(M[e]) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < FCB; ++u) {
-                const int64_t e = e0 + (int64_t)u * SCAN_NT;
+                const int64_t e = e0 + (int64_t)u * FC_NT;
                 if (e >= f1) break;
                 const int r = (int)((tg[u] >> (32 - geo.lk)) & (K - 1));
 #if MISORT_FC_U32
@@ -1297,7 +1306,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // MISORT_FC_SLICES_MAX (tests): the block count from which the coalesced form counts
     static const int64_t slices_max = getenv("MISORT_FC_SLICES_MAX") ? atoll(getenv("MISORT_FC_SLICES_MAX")) : 256;
     if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
-    else k_fence_counts<FT, false><<<(unsigned)nb, SCAN_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
+    else k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
