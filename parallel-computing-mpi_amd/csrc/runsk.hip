@@ -136,11 +136,14 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 // 22 outputs per lane (CAP 10752, three workgroups per CU) measured 2^30
 // 68.9 -> 69.8 Gkeys/s, 2^28 +0.4 %, 2^27 +-0 (profiles/r04/chunk16); 24 per
 // lane (CAP 11776) was 12 % slower.  0 = the 8-way shape for every pass.
+// CAP16 10880 (the largest the 22-output level layout holds: CAP + 8 (G + QA)
+// <= 512 * 22) instead of 10752 with 128-key fences: 2^28 +0.3 %, 2^26
+// +0.8 % (profiles/r05/mergek/cap_ab.txt); the 64-key build keeps 10752.
 #ifndef MISORT_MK_IT16
 #define MISORT_MK_IT16 22
 #endif
 #ifndef MISORT_MK_CAP16
-#define MISORT_MK_CAP16 10752
+#define MISORT_MK_CAP16 10880
 #endif
 #ifndef MISORT_MK_WGCU16
 #define MISORT_MK_WGCU16 3

@@ -5,4 +5,9 @@
 #define MISORT_RUNSK_FGL 6
 #define MISORT_RUNSK_FN(x) x##_fg6
 #define MISORT_RUNSK_SECOND 1
+// 16-way chunk capacity: 10752 keys here (10880, the 128-key build's, measured
+// 2^30 pass +24 us: one more load row per part; profiles/r05/mergek/cap_ab.txt)
+#ifndef MISORT_MK_CAP16
+#define MISORT_MK_CAP16 10752
+#endif
 #include "runsk.hip"
