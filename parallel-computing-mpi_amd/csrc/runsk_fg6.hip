@@ -10,4 +10,9 @@
 #ifndef MISORT_MK_CAP16
 #define MISORT_MK_CAP16 10752
 #endif
+// u64 chunks: 8896 keys (139 fences of 64; the 128-key build's 8832 is 69 of
+// 128): k_mergek -5 us per 2^29 pass (profiles/r05/mergek/cap_ab.txt)
+#ifndef MISORT_MK_CAP64
+#define MISORT_MK_CAP64 8896
+#endif
 #include "runsk.hip"
