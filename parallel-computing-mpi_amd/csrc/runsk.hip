@@ -363,7 +363,10 @@ __global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT
 // end checks.  k_fence_lds ranks every fence by K - 1 binary searches (56
 // dependent LDS reads per fence at K = 8, runs of 256); a merge level costs a
 // lane about 2 log2(S) reads for FIT outputs.
-constexpr int FIT = 8;
+#ifndef MISORT_FENCE_FIT
+#define MISORT_FENCE_FIT 8
+#endif
+constexpr int FIT = MISORT_FENCE_FIT;  // 16: 2^30 pass +11..23 us (profiles/r05/plan/fit_ab.txt)
 template <typename FT>
 __global__ __launch_bounds__(1024) void k_fence_merge(const FT* __restrict__ F, FT* __restrict__ M, int64_t nf,
                                                       int wf_log2, int a) {
