@@ -93,6 +93,12 @@ struct KTr;
 #ifndef MISORT_BOUNDS_LINE
 #define MISORT_BOUNDS_LINE 128
 #endif
+// k_bounds loads the scanned fence counts beside the chunk-start fence (one
+// dependent round less) and divides chunk indices in 32 bits: 2^30 pass -2 to
+// -8 us, 2^28 and u64 equal (profiles/r05/plan/bearly_ab.txt); 0 = before
+#ifndef MISORT_BOUNDS_EARLY
+#define MISORT_BOUNDS_EARLY 1
+#endif
 constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 // u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
 // VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
@@ -292,7 +298,14 @@ struct Geo {
         const int64_t glen = (n - base(g)) < K() * W() ? n - base(g) : K() * W();
         return (glen + FG - 1) >> FG_LOG2;
     }
+#if MISORT_BOUNDS_EARLY
+    // a group's fences and chunks are < 2^31: a 32-bit division
+    __device__ __host__ int64_t nchunks(int64_t g) const {
+        return g < nfull ? kf : (int64_t)((uint32_t)(nfences(g) + fm - 1) / (uint32_t)fm);
+    }
+#else
     __device__ __host__ int64_t nchunks(int64_t g) const { return (nfences(g) + fm - 1) / fm; }
+#endif
     // bounds slot of chunk t of group g (each group has nchunks + 1 slots)
     __device__ __host__ int64_t slot(int64_t g, int64_t t) const {
         return g < nfull ? g * (kf + 1) + t : nfull * (kf + 1) + t;
@@ -662,6 +675,20 @@ __device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<K
     typedef typename KTr<KEY>::F FT;
     const int64_t base = geo.base(g), W = geo.W(), len = geo.run_len(g, r);
     if (t == geo.nchunks(g)) return len;
+#if MISORT_BOUNDS_EARLY
+    // the scanned counts do not depend on the fence: their loads go out with
+    // the fence's (one dependent round less); chunk indices are < 2^31
+    const int K = geo.K();
+    const uint32_t c = (uint32_t)(g * geo.kf + t), c0 = (uint32_t)(g * geo.kf);  // the tail group starts at nfull * kf too
+    const int pc = P[(int64_t)c * K + r] + bsum[(int64_t)(c / (uint32_t)cpb) * K + r];
+    const int pc0 = P[(int64_t)c0 * K + r] + bsum[(int64_t)(c0 / (uint32_t)cpb) * K + r];
+    const FT f = M[(base >> FG_LOG2) + t * geo.fm];
+    const KEY v = (KEY)fkey(f);
+    const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (K - 1));
+    if (r == r0) return (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
+    if (len == 0) return 0;
+    const int64_t lo = (int64_t)pc - pc0;
+#else
     const FT f = M[(base >> FG_LOG2) + t * geo.fm];
     const KEY v = (KEY)fkey(f);
     const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (geo.K() - 1));
@@ -672,6 +699,7 @@ __device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<K
     const int64_t c = g * geo.kf + t, c0 = g * geo.kf;  // the tail group starts at nfull * kf too
     const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / cpb) * K + r]) -
                        (P[c0 * K + r] + bsum[(c0 / cpb) * K + r]);
+#endif
     if (lo <= 0) return 0;  // run r's first key comes after f
     if (lo > (len + FG - 1) >> FG_LOG2) return -1;  // more fences than the run has: malformed input
                                                     // fences; k_chunk_desc rejects the chunk, no read
