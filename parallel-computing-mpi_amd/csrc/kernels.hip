@@ -35,8 +35,11 @@ const PlanKnobs& plan_knobs() {
 int mergek_fence_log2(int64_t n, int key_bytes) {
     // MISORT_FENCE_FG6_MIN (u32) / MISORT_FENCE_FG6_MIN_U64: log2 keys from which
     // the 64-key fences pay (fuller chunks against twice the fences to merge,
-    // count and search; profiles/r05/plan/fg6_ab.txt); 0 = never
-    static const int m32 = getenv("MISORT_FENCE_FG6_MIN") ? atoi(getenv("MISORT_FENCE_FG6_MIN")) : 30;
+    // count and search; profiles/r05/plan/fg6_ab.txt); 0 = never.  Round 6: with
+    // the 12864-key u32 chunks (runsk.hip) a 128-key fence leaves the chunks full
+    // enough, and 64-key fences lose at every u32 size (2^30 85.0 vs 85.8-86.3
+    // Gkeys/s, 2^28/2^29 -3.6 %; profiles/r06/plan/fg6_ab.txt): u32 never, u64 from 2^29
+    static const int m32 = getenv("MISORT_FENCE_FG6_MIN") ? atoi(getenv("MISORT_FENCE_FG6_MIN")) : 0;
     static const int m64 = getenv("MISORT_FENCE_FG6_MIN_U64") ? atoi(getenv("MISORT_FENCE_FG6_MIN_U64")) : 29;
     const int m = key_bytes == 8 ? m64 : m32;
     return m > 0 && m < 63 && n >= ((int64_t)1 << m) ? 6 : MERGEK_FENCE_LOG2;

@@ -138,18 +138,20 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #define MISORT_MK_CHAIN_U64 0
 #endif
 // 16-way u32 passes: larger chunks.  A chunk holds FM * FG = CAP - K * FG
-// keys on average, so at K = 16 a quarter of an 8192-key chunk's lanes idle;
-// 22 outputs per lane (CAP 10752, three workgroups per CU) measured 2^30
-// 68.9 -> 69.8 Gkeys/s, 2^28 +0.4 %, 2^27 +-0 (profiles/r04/chunk16); 24 per
-// lane (CAP 11776) was 12 % slower.  0 = the 8-way shape for every pass.
-// CAP16 10880 (the largest the 22-output level layout holds: CAP + 8 (G + QA)
-// <= 512 * 22) instead of 10752 with 128-key fences: 2^28 +0.3 %, 2^26
-// +0.8 % (profiles/r05/mergek/cap_ab.txt); the 64-key build keeps 10752.
+// keys on average, so at K = 16 a quarter of an 8192-key chunk's lanes idle.
+// Round 4: 22 outputs per lane (CAP 10752, three workgroups per CU) measured
+// 2^30 68.9 -> 69.8 Gkeys/s; 20 or 24 per lane were slower -- an EVEN half
+// (IT / 2 = 10 or 12) puts the lanes' chain pointers, IT / 2 apart, on a few
+// banks.  Round 6: 26 outputs per lane (IT / 2 = 13, odd) and the LDS sized by
+// the larger of the segments and the level outputs (not their sum): CAP 12864,
+// the largest the 26-output level layout holds (CAP + 8 (G + QA) <= 512 * 26),
+// still three workgroups per CU (53.4 KB); 2^30 k_mergek 2154 -> 2049 us,
+// 81.6 -> 84.4 Gkeys/s, 2^28 82.2 -> 84.6 (profiles/r06/mergek/it26_ab.txt).
 #ifndef MISORT_MK_IT16
-#define MISORT_MK_IT16 22
+#define MISORT_MK_IT16 26
 #endif
 #ifndef MISORT_MK_CAP16
-#define MISORT_MK_CAP16 10880
+#define MISORT_MK_CAP16 12864
 #endif
 #ifndef MISORT_MK_WGCU16
 #define MISORT_MK_WGCU16 3
@@ -162,6 +164,24 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_RW16
 #define MISORT_MK_RW16 128
 #endif
+// 16-way u32 passes with bidirectional merge levels (lds_merge_levels_bi):
+// half the workgroup's lanes merge, each IT = MISORT_MK_BI_IT outputs per
+// level from ONE co-rank search at the middle of its range (a chain down and
+// a chain up, interleaved), so a chunk costs half the co-rank searches.
+#ifndef MISORT_MK_BI
+#define MISORT_MK_BI 0
+#endif
+#ifndef MISORT_MK_BI_IT
+#define MISORT_MK_BI_IT 26
+#endif
+#ifndef MISORT_MK_BI_NTM
+#define MISORT_MK_BI_NTM 512  // lanes that merge (whole waves)
+#endif
+// the largest chunk the bidirectional level layout holds (CAP + (K/2)(G + GZ +
+// QA) <= NT/2 * IT with G = IT/2 + 2, GZ = IT/2, QA = IT), or the override
+#ifndef MISORT_MK_CAPBI
+#define MISORT_MK_CAPBI 0
+#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -173,8 +193,13 @@ struct KTr<uint32_t> {
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     // the chunk shape of a pass of lk levels
     static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
-    static constexpr int it(int lk) { return big(lk) ? MISORT_MK_IT16 : IT; }
-    static constexpr int cap(int lk) { return big(lk) ? MISORT_MK_CAP16 : CAP; }
+    static constexpr bool bi(int lk) { return big(lk) && MISORT_MK_BI; }
+    static constexpr int cap_bi() {
+        return MISORT_MK_CAPBI ? MISORT_MK_CAPBI
+                               : MISORT_MK_BI_NTM * MISORT_MK_BI_IT - 8 * (2 * MISORT_MK_BI_IT + 4);
+    }
+    static constexpr int it(int lk) { return bi(lk) ? MISORT_MK_BI_IT : big(lk) ? MISORT_MK_IT16 : IT; }
+    static constexpr int cap(int lk) { return bi(lk) ? cap_bi() : big(lk) ? MISORT_MK_CAP16 : CAP; }
     static constexpr int wg(int lk) { return big(lk) ? MISORT_MK_WGCU16 : WG_PER_CU; }
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = SORT_LT_MERGE, LWK_MAX = 30;  // runs >= the smaller SORT tile; 32-bit row offsets
@@ -205,6 +230,7 @@ struct KTr<uint64_t> {
     static constexpr int WG_PER_CU = MISORT_MK_WGCU64;
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
+    static constexpr bool bi(int) { return false; }
     static constexpr int it(int) { return IT; }
     static constexpr int cap(int) { return CAP; }
     static constexpr int wg(int) { return WG_PER_CU; }
@@ -225,6 +251,9 @@ struct Shape {
     // after each sequence: G >= the keys a chain may read past its sequence
     static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
     static constexpr int NT = T::NT, IT = T::it(LK), CAP = T::cap(LK);
+    static constexpr bool BI = T::bi(LK);  // bidirectional levels (lds_merge_levels_bi)
+    static constexpr int NTM = BI ? MISORT_MK_BI_NTM : NT;  // lanes that merge
+    static_assert(NTM % 64 == 0 && NTM <= NT, "merging lanes: whole waves");
     static constexpr int MAXR = CAP / 2;  // co-rank range bound: min(LA, LB) <= CAP / 2
     // chain 3 merges RN = IT + 2 keys rounded up to even (the lane's IT outputs
     // after up to two early keys) and reads up to RN + 2 - 2 keys past a
@@ -235,14 +264,20 @@ struct Shape {
     // one's, so G exceeds the keys a chain reads past a sequence (IT for the
     // two-key chains, IT + 1 for the one-key chain)
     static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2 || (CH == 0 && MISORT_MK_ZW_CH0));
-    static constexpr int G = CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
+    // BI: a lane's outputs below / above its split (lds_merge_levels_bi)
+    static constexpr int BID = IT % 4 ? IT / 2 - 1 : IT / 2, BIU = IT - BID;
+    static constexpr int G = BI ? BIU + 2 : CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
+    static constexpr int GZ = BI ? BID : 0;  // BI: zero words below every sequence
     // level outputs start at lane boundaries; chain 3 also needs even slots
     static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
+    static_assert(!BI || (CH == 1 || CH == 2), "bidirectional levels: two-key chains");
     static_assert(CH != 3 || QA % 2 == 0, "chain 3: even sequence starts");
     static_assert(CH == 3 || IT % 2 == 0, "chains 0-2: outputs stored as aligned pairs");
     // LDS slot of segment q (o = its first chunk position): chain 3 reads
     // aligned pairs, so every sequence starts at an even slot
-    __device__ __host__ static int seg(int o, int q) { return CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G; }
+    __device__ __host__ static int seg(int o, int q) {
+        return BI ? o + q * (G + GZ) : CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G;
+    }
     static constexpr int K = 1 << LK, LKS = LK;
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
     static constexpr int RW = LK == 4 ? MISORT_MK_RW16 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
@@ -250,16 +285,25 @@ struct Shape {
     // load slots per lane: enough rows for CAP keys in K segments (18 at
     // CAP = 8192, IT = 17 or 18)
     static constexpr int LS_ROWS = ((CAP + RW - 1) / RW + K + NR - 1) / NR;
-    static constexpr int LS = ((IT + 1) & ~1) > LS_ROWS ? ((IT + 1) & ~1) : LS_ROWS;
+    static constexpr int LS = BI || ((IT + 1) & ~1) <= LS_ROWS ? LS_ROWS : ((IT + 1) & ~1);
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
-    static constexpr int LDS_KEYS = PAD + CAP + K * (G + QA) + 16;
+    // keys below s (a co-rank probe may read index -1; BI: the zero words
+    // below the first sequence), a multiple of 4 keeps s 16-byte aligned
+    static constexpr int PADK = BI ? (GZ + 3) / 4 * 4 : PAD;
+    static constexpr int BI_EXT = CAP + K * (G + GZ) > NTM * IT + G ? CAP + K * (G + GZ) : NTM * IT + G;
+    // the tile holds the chunk's segments with their sentinels (CAP + K G) and
+    // every level's outputs (<= NT IT slots by the level layout, + G sentinels)
+    static constexpr int NB_EXT = CAP + K * G > NT * IT + G ? CAP + K * G : NT * IT + G;
+    static constexpr int LDS_KEYS = BI ? PADK + BI_EXT + 16 : CH == 3 ? PAD + CAP + K * (G + QA) + 16 : PAD + NB_EXT + 16;
     // the levels' pair table in LDS (MISORT_MK_PT)
     static constexpr bool PT = MISORT_MK_PT && K > 2;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
-    static_assert(CAP + (K / 2) * (G + QA) <= NT * IT, "level layout: pairs at lane boundaries");
-    static_assert(PAD + CAP + K * (G + QA) < 65536, "LDS key index of a row fits 16 bits");
+    static_assert(BI ? CAP + (K / 2) * (G + GZ + QA) <= NTM * IT : CAP + (K / 2) * (G + QA) <= NT * IT,
+                  "level layout: pairs at lane boundaries");
+    static_assert(LDS_KEYS < 65536, "LDS key index of a row fits 16 bits");
+    static_assert(!BI || G + GZ <= 64, "sentinels: one wave per segment");
 };
 
 // fence <-> (key, tag): tag = run << (32 - lk) | position / FG, the low 32 bits
@@ -1033,7 +1077,7 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NT = S::NT, IT = S::IT;
     constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
-    constexpr int LAST = S::LDS_KEYS - PAD - 1;
+    constexpr int LAST = S::LDS_KEYS - S::PADK - 1;
     const int len = d->o[K];
     constexpr int RN = S::RN;  // chain 3: up to two leading keys not the lane's (ex)
     KEY r[RN];
@@ -1046,7 +1090,8 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
         st[q] = S::seg(d->o[q], q);
         ln[q] = d->o[q + 1] - d->o[q];
     }
-    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
+    if constexpr (S::BI) lds_merge_levels_bi<KEY, S>(s, st, ln, r, ex, tid);
+    else lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
     const int64_t out0 = d->out0;
     // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
@@ -1059,6 +1104,9 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
             // 16-byte) write per two keys instead of one write per key
 #pragma unroll
             for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(q + j) = kvec2<KEY>{r[j], r[j + 1]};
+        } else if constexpr (S::BI) {
+#pragma unroll
+            for (int k = 0; k < IT; ++k) q[k] = r[k];
         } else {
 #pragma unroll
             for (int k = 0; k < RN; ++k)
@@ -1101,6 +1149,15 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
     // by scalar loads), G <= 64 lanes each
     static_assert(S::G <= 64, "sentinels: one wave per segment");
     const int lane = tid & 63;
+    if constexpr (S::BI) {
+        // G MAX words above each segment, GZ zero words below it
+        for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64) {
+            const int b = S::seg(d->o[q], q);
+            if (lane < S::G) s[b + (d->o[q + 1] - d->o[q]) + lane] = KMAX<KEY>;
+            else if (lane < S::G + S::GZ) s[b - S::GZ + (lane - S::G)] = (KEY)0;
+        }
+        return;
+    }
     for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64)
         if (lane < S::G)
             s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = S::ZW && lane == S::G - 1 ? (KEY)0 : KMAX<KEY>;
@@ -1133,7 +1190,7 @@ __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256)
     __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
     __shared__ PairRec ptab[S::PT ? S::K / 2 : 1];
     PairRec* pt = S::PT ? ptab : nullptr;
-    KEY* s = tile + PAD;
+    KEY* s = tile + S::PADK;
     const int tid = threadIdx.x;
     uint32_t chunk = blockIdx.x;
     if constexpr (MISORT_MK_XCD) {

@@ -5,11 +5,6 @@
 #define MISORT_RUNSK_FGL 6
 #define MISORT_RUNSK_FN(x) x##_fg6
 #define MISORT_RUNSK_SECOND 1
-// 16-way chunk capacity: 10752 keys here (10880, the 128-key build's, measured
-// 2^30 pass +24 us: one more load row per part; profiles/r05/mergek/cap_ab.txt)
-#ifndef MISORT_MK_CAP16
-#define MISORT_MK_CAP16 10752
-#endif
 // u64 chunks: 8896 keys (139 fences of 64; the 128-key build's 8832 is 69 of
 // 128): k_mergek -5 us per 2^29 pass (profiles/r05/mergek/cap_ab.txt)
 #ifndef MISORT_MK_CAP64

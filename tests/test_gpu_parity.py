@@ -308,21 +308,37 @@ def test_past_the_multiway_limit_u64(ctx):
     assert a[:3] == b[:3] and torch.equal(a[3], b[3])
 
 
-def test_f64_signed_zeros_total_order(ctx):
-    """-0.0 == +0.0 as doubles: std::sort (psort.cc:175) leaves their relative
-    order unspecified and compare_split keeps whichever side its '<'/'>' picks,
-    so the reference's bits for such mixtures are not defined.  This build
-    sorts by the order-preserving u64 map (a total order: -0.0 before +0.0),
-    documented in include/misort.h; the output is a permutation that is
-    non-decreasing as doubles and equals the oracle's (same total order)."""
-    rng = np.random.default_rng(3)
-    x = np.concatenate([np.zeros(500), -np.zeros(500), rng.standard_normal(3000), [1e-300, -1e-300]])
-    rng.shuffle(x)
-    d = to_dev(x)
-    ctx.local_sort(d)
-    y = to_host(d, np.float64)
-    assert np.all(y[1:] >= y[:-1])
+F64Z = json.load(open(os.path.join(GOLD_DIR, "f64zero.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", F64Z, ids=lambda c: f"P{c['p']}")
+def test_f64_signed_zeros_vs_reference(ctx, case):
+    """-0.0 / +0.0 mixtures against the compiled reference's own output
+    (tests/golden/make_golden_f64zero.py: parallel_bitonic_sort, psort.cc:167-201,
+    at P = 1, 2, 4, 8 on the same 4002 doubles).  The reference writes its 1000
+    zeros in an implementation-defined sign order (std::sort and the strict
+    '<'/'>' merges, psort.cc:128-137,153-162: 487-515 sign changes across P);
+    this build sorts by the order-preserving u64 map (-0.0 before +0.0 within a
+    rank's block, include/misort.h).  Pinned against the reference: every
+    position equal as a double, every non-zero position bit-exact, the same
+    per-rank sizes and check_sort count, and the output a permutation of the
+    input's bit patterns.  The measured deviation (zero positions whose sign
+    differs) is reported, not asserted to be zero."""
+    x = np.fromfile(os.path.join(GOLD_DIR, "f64zero.in"))
+    ref = np.fromfile(os.path.join(GOLD_DIR, f"f64zero_P{case['p']}.out"))
+    assert sha(ref) == case["out_sha256"]
+    y = virtual_ranks(ctx, x, case["p"])
+    assert np.array_equal(y, ref)  # as doubles: -0.0 == +0.0
+    nz = ref != 0
+    np.testing.assert_array_equal(y.view(np.uint64)[nz], ref.view(np.uint64)[nz])
     np.testing.assert_array_equal(np.sort(y.view(np.uint64)), np.sort(x.view(np.uint64)))
-    np.testing.assert_array_equal(y.view(np.uint64), O.local_sort(x).view(np.uint64))
-    zeros = y[(y == 0)]
-    assert np.all(np.signbit(zeros[:500])) and not np.any(np.signbit(zeros[500:]))
+    assert O.check_sort(y, case["p"]) == case["errors"]
+    sizes = misort.block_sizes(x.size, case["p"])
+    assert list(sizes) == case["sizes"]
+    # within each rank's block this build's zeros are -0.0 first
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    for r in range(case["p"]):
+        z = np.signbit(y[offs[r]:offs[r + 1]][y[offs[r]:offs[r + 1]] == 0])
+        assert np.all(z[:z.sum()]) and not np.any(z[z.sum():])
+    differ = int(np.count_nonzero(y.view(np.uint64) != ref.view(np.uint64)))
+    print(f"P={case['p']}: {differ} of {case['zeros']} zero positions differ in sign from the reference")

@@ -221,7 +221,7 @@ ctx.close()
     (4, {"MISORT_FENCE_NEST_MIN": "12"}, (1 << 27) + 777),
     (4, {"MISORT_FENCE_NEST_MIN": "12", "MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),
     (4, {"MISORT_FENCE_NEST_MIN": "0"}, (1 << 27) + 777),  # never nested
-    # 64-key fences (runsk_fg6.hip; the default from 2^30 u32 / 2^29 u64 keys)
+    # 64-key fences (runsk_fg6.hip; the default from 2^29 u64 keys, forced here for u32)
     (4, {"MISORT_FENCE_FG6_MIN": "20"}, (1 << 26) + 12345),
     (4, {"MISORT_FENCE_FG6_MIN": "20"}, (1 << 27) + 777),
     (4, {"MISORT_FENCE_FG6_MIN": "20", "MISORT_FENCE_NEST_MIN": "12"}, (1 << 26) + 12345),

@@ -144,3 +144,23 @@ def test_u64mix_is_split_invariant_and_mixed():
     assert 0.03 < np.mean(x == 0) < 0.07 and 0.03 < np.mean(x == np.uint64(O.ALL_ONES)) < 0.07
     r = O.u64mix(0x5EED0005, n, top=O.REF_TOP)
     assert r.max() <= np.uint64(O.REF_TOP)
+
+
+F64Z = json.load(open(os.path.join(GOLD_DIR, "f64zero.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", F64Z, ids=lambda c: f"P{c['p']}")
+def test_f64_signed_zero_fixtures(case):
+    """The oracle on the reference's +-0.0 fixtures (make_golden_f64zero.py):
+    equal as doubles at every position, bit-exact wherever the value is not
+    zero, the same check_sort count; only the zeros' sign order is the
+    reference's implementation-defined one (parity unpinned for those bits)."""
+    x = np.fromfile(os.path.join(GOLD_DIR, "f64zero.in"))
+    ref = np.fromfile(os.path.join(GOLD_DIR, f"f64zero_P{case['p']}.out"))
+    assert sha(ref) == case["out_sha256"]
+    y = O.parallel_bitonic_sort(x, case["p"])
+    assert np.array_equal(y, ref)
+    nz = ref != 0
+    np.testing.assert_array_equal(y.view(np.uint64)[nz], ref.view(np.uint64)[nz])
+    assert O.check_sort(y, case["p"]) == case["errors"]
+    assert int(np.count_nonzero(ref == 0)) == case["zeros"]
