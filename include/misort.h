@@ -71,8 +71,12 @@ enum misort_kernel_kind {
     MISORT_K_EXCHANGE = 8,    /* compare-split exchange leg (splitter samples, RCCL
                                  send/recv, codec), device time between events */
     MISORT_K_RUN_MERGE4 = 9,  /* a multi-way pass: lk merge levels, runs 2^hi -> 2^(hi+lk) */
-    MISORT_K_RUN_MERGEK_KERNEL = 10 /* the merge kernel of a multi-way pass alone (its planning
-                                       kernels excluded; nested in MISORT_K_RUN_MERGE4) */
+    MISORT_K_RUN_MERGEK_KERNEL = 10, /* the merge kernel of a multi-way pass alone (its planning
+                                        kernels excluded; nested in MISORT_K_RUN_MERGE4) */
+    MISORT_K_MERGE_SPLIT_TAIL = 11  /* in-place compare-split of a small bracket
+                                       (misort_merge_split_tail); its bytes are an UPPER bound,
+                                       2 nblock + min(nblock, nrecv) keys: the device finds the
+                                       window it rewrites */
 };
 
 typedef struct misort_ctx misort_ctx;
@@ -185,6 +189,16 @@ int misort_parallel_sample_sort(misort_ctx* ctx, int dtype, const void* d_in, vo
 int misort_merge_split(misort_ctx* ctx, int dtype, const void* d_local, int64_t nloc,
                        const void* d_recv, int64_t nrecv, void* d_out, int keep_max,
                        void* stream);
+
+/* The same keep-n merge IN PLACE (psort.cc:116-164, the result replaces
+ * d_block): the path a hypercube stage takes when the partner's bracket k is
+ * small (k <= nblock / MISORT_TAIL_DIV, default 8): only the end of the block
+ * that the nrecv received keys reach is rewritten, staged through the context's
+ * work buffer.  d_recv must not overlap d_block (MISORT_E_INVALID).  Exposed
+ * so the path is testable on its own (extension; the reference merges the
+ * whole block every stage). */
+int misort_merge_split_tail(misort_ctx* ctx, int dtype, void* d_block, int64_t nblock,
+                            const void* d_recv, int64_t nrecv, int keep_max, void* stream);
 
 /* psort.cc:497-520 check_sort: local descents of this rank's block plus the
  * boundary descent against rank-1's last key, summed over the communicator.

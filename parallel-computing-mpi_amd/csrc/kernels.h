@@ -36,7 +36,9 @@ enum Kind : int {
     KIND_EXCHANGE = 8,    // compare-split exchange leg (samples, RCCL send/recv, codec); not a kernel
     KIND_RUNSK = 9,       // R merge levels in one pass: runs of 2^hi -> 2^(hi+R), 2^R-way (runsk.hip)
     KIND_RUNSK_KERNEL = 10,  // the k_mergek launch of a KIND_RUNSK pass alone (nested in it)
-    KIND_COUNT = 11
+    KIND_MERGE_SPLIT_TAIL = 11,  // in-place compare-split of a small bracket; bytes: an UPPER bound
+                                 // (2 na + min(na, nb) keys: the device finds the window it rewrites)
+    KIND_COUNT = 12
 };
 
 // Per-launch hook: called before and after every kernel launch of a sort with

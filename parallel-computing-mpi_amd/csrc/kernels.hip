@@ -434,7 +434,9 @@ hipError_t merge_split_tail(K* a, int64_t na, const K* b, int64_t nb, int keep_m
                             hipStream_t s, LaunchHook* hook) {
     if (na <= 0) return hipSuccess;
     const int64_t ntiles = (na + MS_TILE - 1) / MS_TILE;  // the worst case, W = na
-    HookScope hs(hook, KIND_MERGE_SPLIT, (double)(2 * na + (nb < na ? nb : na)) * sizeof(K), s);
+    // its own kind: the window (found on the device) is usually far smaller
+    // than the block, so these bytes are only an upper bound
+    HookScope hs(hook, KIND_MERGE_SPLIT_TAIL, (double)(2 * na + (nb < na ? nb : na)) * sizeof(K), s);
     int64_t* win = scratch;
     int64_t* co = scratch + 4;
     k_tail_window<K><<<1, TW_NT, 0, s>>>(a, na, b, nb, keep_max, win);

@@ -1253,7 +1253,13 @@ std::map<std::pair<int, hipStream_t>, Scratch> g_scr[4];
 // which = 0: the two fence buffers (a pass's input fences are the previous
 // pass's output: sized by n alone, so they never move between the passes of
 // one sort); which = 1: per-pass planning data (free to grow at any pass);
-// 2 and 3: the same for a pass nested in a pass's fence merge (depth 1).
+// 2 and 3: the same for a pass nested in a pass's fence merge (depth 1).  The
+// depth-1 sets are sized by the nested pass's n (the outer pass's fence count)
+// and may grow once, on the first nested pass of a new larger sort -- partway
+// through that sort, after the outer pass's first planning launches are
+// queued: growth synchronises the stream before it frees (a latency cost, the
+// queued work never sees a freed buffer), and the depth-1 fence buffers are
+// only ever read by the nested pass that wrote them.
 void* scratch(int which, size_t bytes, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;

@@ -757,6 +757,16 @@ struct LocalTransport final : Transport {
     }
 };
 
+// MISORT_TAIL_DIV: a stage whose k received keys are at most 1/tail_div of the
+// block merges in place at the block's end (0 = never); clamped to [0, 2^20]
+// so the bracket test cannot overflow.
+int64_t env_tail_div() {
+    const char* v = getenv("MISORT_TAIL_DIV");
+    if (!v) return 8;
+    const long long d = atoll(v);
+    return d < 0 ? 0 : d > (1 << 20) ? (1 << 20) : (int64_t)d;
+}
+
 }  // namespace
 
 struct misort_ctx {
@@ -787,7 +797,7 @@ struct misort_ctx {
     // a stage whose message is at most 1/tail_div of the block merges in place
     // at the block's end (misort::merge_split_tail); 0 = always the
     // whole-block merge (MISORT_TAIL_DIV)
-    int64_t tail_div = getenv("MISORT_TAIL_DIV") ? atoll(getenv("MISORT_TAIL_DIV")) : 8;
+    int64_t tail_div = env_tail_div();
     DevBuf enc_send, enc_recv, codec_scr;
     int64_t xchg_raw_bytes = 0;  // what the coded stages would have moved uncoded
     ~misort_ctx() {
@@ -915,6 +925,10 @@ int do_merge_split_tail(misort_ctx* c, int dtype, void* a, int64_t na, const voi
     if (e != hipSuccess) return fail(MISORT_E_HIP, "merge_split_tail: %s", hipGetErrorString(e));
     return MISORT_OK;
 }
+
+// The small-bracket test of a hypercube stage: k received keys against a block
+// of loc (k <= loc / tail_div, no product to overflow).
+bool tail_bracket(const misort_ctx* c, int64_t k, int64_t loc) { return c->tail_div > 0 && k <= loc / c->tail_div; }
 
 // Splitter samples of a sorted block: a[min(c*S, n-1)], c = 0..ceil(n/S).
 int64_t sample_stride(int64_t n) { return std::max<int64_t>(256, (n + 32767) / 32768); }
@@ -1277,7 +1291,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
                 continue;
             }
             xg_close((double)(c->xchg_bytes - moved0));
-            if (c->tail_div > 0 && k * c->tail_div <= loc) {
+            if (tail_bracket(c, k, loc)) {
                 // a small bracket: rewrite only the end of the block it reaches
                 if ((rc = do_merge_split_tail(c, dtype, cur, loc, rkeys, k, other, keep[st], s))) return rc;
                 continue;
@@ -1334,7 +1348,7 @@ int parallel_sort(misort_ctx* c, int dtype, const void* in, void* out, int64_t l
         c->xchg_bytes += (int64_t)(sbytes + rbytes);
         c->xchg_raw_bytes += (int64_t)(sbytes + rbytes);
         xg_close((double)(c->xchg_bytes - moved0));
-        if (k > 0 && c->tail_div > 0 && k * c->tail_div <= loc) {
+        if (k > 0 && tail_bracket(c, k, loc)) {
             if ((rc = do_merge_split_tail(c, dtype, cur, loc, rkeys, nrecv, other, keep[st], s))) return rc;
             continue;
         }
@@ -1943,18 +1957,7 @@ int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc
     if (!c || !valid_dtype(dtype) || nloc < 0 || nrecv < 0)
         return fail(MISORT_E_INVALID, "bad merge_split arguments");
     hipStream_t s = pick(c, stream);
-    if (dtype != MISORT_F64) {
-        // MISORT_MERGE_SPLIT_TAIL=1 (tests): the in-place tail merge the
-        // hypercube stages use for small brackets, on a copy of local in out
-        const char* tail = getenv("MISORT_MERGE_SPLIT_TAIL");
-        if (tail && atoi(tail) != 0 && nloc > 0) {
-            int rc = c->work.ensure((size_t)nloc * key_bytes(dtype));
-            if (rc) return rc;
-            if (out != local) HIPCHK(hipMemcpyAsync(out, local, (size_t)nloc * key_bytes(dtype), hipMemcpyDeviceToDevice, s));
-            return do_merge_split_tail(c, dtype, out, nloc, recv, nrecv, c->work.p, keep_max, s);
-        }
-        return do_merge_split(c, dtype, local, nloc, recv, nrecv, out, keep_max, s);
-    }
+    if (dtype != MISORT_F64) return do_merge_split(c, dtype, local, nloc, recv, nrecv, out, keep_max, s);
     // f64: order-preserving copies of both blocks, merge, map back.
     int rc;
     if ((rc = c->work.ensure(std::max<size_t>(8, (size_t)nloc * 8)))) return rc;
@@ -1965,6 +1968,33 @@ int misort_merge_split(misort_ctx* c, int dtype, const void* local, int64_t nloc
     HIPCHK(misort::f64_to_ord((uint64_t*)c->recv.p, nrecv, s));
     if ((rc = do_merge_split(c, dtype, c->work.p, nloc, c->recv.p, nrecv, out, keep_max, s))) return rc;
     HIPCHK(misort::ord_to_f64((uint64_t*)out, nloc, s));
+    return MISORT_OK;
+}
+
+int misort_merge_split_tail(misort_ctx* c, int dtype, void* block, int64_t nblock, const void* recv, int64_t nrecv,
+                            int keep_max, void* stream) {
+    if (!c || !valid_dtype(dtype) || nblock < 0 || nrecv < 0 || (nblock > 0 && !block) || (nrecv > 0 && !recv))
+        return fail(MISORT_E_INVALID, "bad merge_split_tail arguments");
+    if (nblock > 0 && nrecv > 0) {
+        // the received run must not overlap the block rewritten in place
+        const char *b0 = (const char*)block, *b1 = b0 + nblock * key_bytes(dtype);
+        const char *r0 = (const char*)recv, *r1 = r0 + nrecv * key_bytes(dtype);
+        if (r0 < b1 && b0 < r1) return fail(MISORT_E_INVALID, "merge_split_tail: recv overlaps the block");
+    }
+    if (nblock == 0) return MISORT_OK;
+    hipStream_t s = pick(c, stream);
+    int rc;
+    // the staging buffer: the context's work buffer (a block's worth)
+    if ((rc = c->work.ensure((size_t)nblock * key_bytes(dtype)))) return rc;
+    if (dtype != MISORT_F64) return do_merge_split_tail(c, dtype, block, nblock, recv, nrecv, c->work.p, keep_max, s);
+    // f64 (the ordered form the hypercube stages merge in): the block mapped
+    // in place, the received keys as an ordered copy, mapped back after
+    if ((rc = c->recv.ensure(std::max<size_t>(8, (size_t)nrecv * 8)))) return rc;
+    HIPCHK(hipMemcpyAsync(c->recv.p, recv, (size_t)nrecv * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(misort::f64_to_ord((uint64_t*)block, nblock, s));
+    HIPCHK(misort::f64_to_ord((uint64_t*)c->recv.p, nrecv, s));
+    if ((rc = do_merge_split_tail(c, dtype, block, nblock, c->recv.p, nrecv, c->work.p, keep_max, s))) return rc;
+    HIPCHK(misort::ord_to_f64((uint64_t*)block, nblock, s));
     return MISORT_OK;
 }
 

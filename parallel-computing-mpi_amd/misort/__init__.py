@@ -24,7 +24,7 @@ __all__ = [
 
 U32, U64, F64 = 0, 1, 2
 KIND_NAMES = ["tile_sort", "global_pass", "tile_merge", "merge_split", "other", "span_pass",
-              "wide_pass", "run_merge", "exchange", "run_mergek", "run_mergek_kernel"]
+              "wide_pass", "run_merge", "exchange", "run_mergek", "run_mergek_kernel", "merge_split_tail"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.environ.get("MISORT_LIBRARY") or os.path.join(os.path.dirname(_HERE), "lib", "libmisort.so")
@@ -77,6 +77,7 @@ def lib():
         "misort_parallel_bitonic_sort_oop": ([vp, i32, vp, vp, i64, i64, vp], i32),
         "misort_local_sort": ([vp, i32, vp, vp, i64, vp], i32),
         "misort_merge_split": ([vp, i32, vp, i64, vp, i64, vp, i32, vp], i32),
+        "misort_merge_split_tail": ([vp, i32, vp, i64, vp, i64, i32, vp], i32),
         "misort_parallel_quick_sort": ([vp, i32, vp, i64, vp, i64, ctypes.POINTER(i64), vp], i32),
         "misort_parallel_sample_sort": ([vp, i32, vp, vp, i64, i64, vp], i32),
         "misort_check_sort": ([vp, i32, vp, i64, ctypes.POINTER(i64), vp], i32),
@@ -352,10 +353,18 @@ class Context:
                                        self._stream(stream)))
         return out
 
-    def compare_split(self, local, recv, keep_max, out=None, stream=None):
-        """Device half of psort.cc:116-164 (no exchange)."""
+    def compare_split(self, local, recv, keep_max, out=None, stream=None, in_place_tail=False):
+        """Device half of psort.cc:116-164 (no exchange).  in_place_tail: the
+        small-bracket path of the hypercube stages (misort_merge_split_tail) on a
+        copy of `local` in `out`."""
         import torch
         out = torch.empty_like(local) if out is None else out
+        if in_place_tail:
+            if out.data_ptr() != local.data_ptr():
+                out[:local.numel()].copy_(local)
+            _check(lib().misort_merge_split_tail(self._h, _dtype_of(local), _ptr(out), local.numel(),
+                                                 _ptr(recv), recv.numel(), int(keep_max), self._stream(stream)))
+            return out
         _check(lib().misort_merge_split(self._h, _dtype_of(local), _ptr(local), local.numel(),
                                         _ptr(recv), recv.numel(), _ptr(out), int(keep_max),
                                         self._stream(stream)))

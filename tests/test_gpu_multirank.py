@@ -56,10 +56,11 @@ def to_host(t, dtype):
     return t.cpu().numpy()
 
 
-def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compress=True, raw=None):
+def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compress=True, raw=None, kinds=None):
     """Each rank sorts its reference-layout block; returns (concatenated
     result, check_sort count of every rank, exchange stats of every rank).
-    raw (a dict) receives each rank's uncoded exchange bytes."""
+    raw (a dict) receives each rank's uncoded exchange bytes; kinds (a dict)
+    each rank's profiled launches per kernel kind."""
     sizes = misort.block_sizes(x.size, p)
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     max_size = x.size // p + 1
@@ -72,8 +73,14 @@ def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compre
         buf = to_dev(np.concatenate([blocks[r], np.zeros(max_size - sizes[r], x.dtype)]))
         out = torch.empty_like(buf) if out_of_place else None
         torch.cuda.synchronize()
+        if kinds is not None:
+            ctx.profile(True)
+            ctx.profile_reset()
         res = ctx.parallel_bitonic_sort(buf, sizes[r], max_size, out=out, stream=ctx.native_stream)
         ctx.synchronize()
+        if kinds is not None:
+            kinds[r] = {k: v[0] for k, v in ctx.profile_read().items()}
+            ctx.profile(False)
         errs = ctx.check_sort(res, sizes[r], stream=ctx.native_stream)
         if out_of_place:  # input left unchanged
             np.testing.assert_array_equal(to_host(buf[:sizes[r]], x.dtype), blocks[r])
@@ -185,6 +192,28 @@ def test_f64_psort_generator_group_p8_large():
     want = O.parallel_bitonic_sort(x, 8)
     np.testing.assert_array_equal(y.view(np.uint64), want.view(np.uint64))
     assert errs == [O.check_sort(want, 8)] * 8
+
+
+@pytest.mark.parametrize("kind", ["u32", "f64"])
+def test_tail_merges_vs_whole_block(monkeypatch, kind):
+    """The hypercube stages with the in-place small-bracket compare-split
+    (MISORT_TAIL_DIV = 8, the default: k <= loc / 8) and with whole-block
+    merges only (0) write the same bytes as the oracle (psort.cc:116-201), for
+    u32 and for f64 (the stages merge the ordered form; the last one maps back
+    to double bits); the default run takes the tail path at least once."""
+    p = 8
+    n = (1 << 20) + 5
+    x = O.splitmix(0x5EED7A11, n, np.uint32) if kind == "u32" else O.generate_f64(n)
+    want = O.parallel_bitonic_sort(x, p)
+    w = np.uint64 if kind == "f64" else np.uint32
+    for div, tail in (("0", False), ("8", True)):
+        monkeypatch.setenv("MISORT_TAIL_DIV", div)
+        kinds = {}
+        y, errs, _ = group_sort(x, p, kinds=kinds)
+        np.testing.assert_array_equal(y.view(w), want.view(w))
+        assert errs == [O.check_sort(want, p)] * p
+        ntail = sum(k.get("merge_split_tail", 0) for k in kinds.values())
+        assert (ntail > 0) == tail, (div, ntail)
 
 
 def _u64_mix(n, seed):

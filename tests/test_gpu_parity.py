@@ -131,15 +131,14 @@ def test_merge_split(ctx, na, nb, keep_max):
 @pytest.mark.parametrize("case", ["tail", "head", "overlap", "dups", "wide"])
 @pytest.mark.parametrize("na,nb", [(1, 1), (4097, 3), (100000, 4096), (1 << 20, 777)])
 @pytest.mark.parametrize("keep_max", [0, 1])
-@pytest.mark.parametrize("kd", [np.uint32, np.uint64])
-def test_merge_split_tail(ctx, monkeypatch, case, na, nb, keep_max, kd):
+@pytest.mark.parametrize("kd", [np.uint32, np.uint64, np.float64])
+def test_merge_split_tail(ctx, case, na, nb, keep_max, kd):
     """The in-place compare-split of a small bracket (merge_split_tail: only
     the end of the block the partner's keys reach is rewritten) against the
     oracle's keep-n merge (psort.cc:116-164).  The partner's keys sit at the
     block's far end (tail: the usual small-bracket stage), straddle all of it
     (wide: the window is the whole block), duplicate its boundary keys, or
     overlap its middle."""
-    monkeypatch.setenv("MISORT_MERGE_SPLIT_TAIL", "1")
     big = 1 << 30 if kd == np.uint32 else 1 << 60
     a = O.local_sort((O.splitmix(na * 5 + 2, na, np.uint64) % big).astype(kd))
     r = O.splitmix(nb * 3 + 9, nb, np.uint64)
@@ -159,8 +158,9 @@ def test_merge_split_tail(ctx, monkeypatch, case, na, nb, keep_max, kd):
     if lo is not None:
         b = O.local_sort((lo + r % max(1, hi - lo)).astype(kd))
     want = O.compare_split(a, b, keep_max)
-    out = ctx.compare_split(to_dev(a), to_dev(b), keep_max)
-    np.testing.assert_array_equal(to_host(out, kd), want)
+    out = ctx.compare_split(to_dev(a), to_dev(b), keep_max, in_place_tail=True)
+    np.testing.assert_array_equal(to_host(out, kd).view(np.uint64 if kd == np.float64 else kd),
+                                  want.view(np.uint64 if kd == np.float64 else kd))
 
 
 @pytest.mark.parametrize("keep_max", [0, 1])

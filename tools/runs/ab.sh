@@ -36,8 +36,15 @@ PY
 done
 for p in $PROF; do
   L=${p%%:*}; dt=${p##*:}
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${dt}_$L" -o run -- python3 -u bench.py --dtype $dt --logn $L --steps 10 --warmup 3 --no-cpu-baseline \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${dt}_$L" -o run --output-format csv -- python3 -u bench.py --dtype $dt --logn $L --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline \
     > "$O/prof_${dt}_$L.json" 2> "$O/prof_${dt}_$L.err"; fatal $? "rocprof $p"
   find "$O/prof_${dt}_$L" -name "*kernel_stats.csv" -exec cp {} "$O/prof_${dt}_${L}_kernel_stats.csv" \;
+  find "$O/prof_${dt}_$L" -name "*.db" -delete
+  python3 - "$O/prof_${dt}_${L}_kernel_stats.csv" <<'PY'
+import csv, sys
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:8]:
+    print("rocprof", r["Name"].split("(")[0][-50:], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+PY
 done
 echo done
