@@ -193,13 +193,17 @@ struct KTr<uint32_t> {
     static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
     // the chunk shape of a pass of lk levels
     static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
+    static constexpr int nt(int) { return NT; }
     static constexpr bool bi(int lk) { return big(lk) && MISORT_MK_BI; }
     static constexpr int cap_bi() {
         return MISORT_MK_CAPBI ? MISORT_MK_CAPBI
                                : MISORT_MK_BI_NTM * MISORT_MK_BI_IT - 8 * (2 * MISORT_MK_BI_IT + 4);
     }
     static constexpr int it(int lk) { return bi(lk) ? MISORT_MK_BI_IT : big(lk) ? MISORT_MK_IT16 : IT; }
-    static constexpr int cap(int lk) { return bi(lk) ? cap_bi() : big(lk) ? MISORT_MK_CAP16 : CAP; }
+    // (k_fence_counts keeps 8-bit per-chunk counts: at most 255 + K fences of FG
+    // keys a chunk, a bound only the 64-key build can reach)
+    static constexpr int cap16() { return MISORT_MK_CAP16 < (255 + 16) * FG ? MISORT_MK_CAP16 : (255 + 16) * (int)FG; }
+    static constexpr int cap(int lk) { return bi(lk) ? cap_bi() : big(lk) ? cap16() : CAP; }
     static constexpr int wg(int lk) { return big(lk) ? MISORT_MK_WGCU16 : WG_PER_CU; }
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = SORT_LT_MERGE, LWK_MAX = 30;  // runs >= the smaller SORT tile; 32-bit row offsets
@@ -231,6 +235,7 @@ struct KTr<uint64_t> {
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
     static constexpr bool bi(int) { return false; }
+    static constexpr int nt(int) { return NT; }
     static constexpr int it(int) { return IT; }
     static constexpr int cap(int) { return CAP; }
     static constexpr int wg(int) { return WG_PER_CU; }
@@ -250,7 +255,7 @@ struct Shape {
     // the merge chain of the in-LDS levels (MISORT_MK_CHAIN*) and the sentinels
     // after each sequence: G >= the keys a chain may read past its sequence
     static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
-    static constexpr int NT = T::NT, IT = T::it(LK), CAP = T::cap(LK);
+    static constexpr int NT = T::nt(LK), IT = T::it(LK), CAP = T::cap(LK);
     static constexpr bool BI = T::bi(LK);  // bidirectional levels (lds_merge_levels_bi)
     static constexpr int NTM = BI ? MISORT_MK_BI_NTM : NT;  // lanes that merge
     static_assert(NTM % 64 == 0 && NTM <= NT, "merging lanes: whole waves");
@@ -1183,7 +1188,7 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
 template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
-__global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256) void k_mergek(
+__global__ __launch_bounds__(KTr<KEY>::nt(LK), KTr<KEY>::wg(LK)* KTr<KEY>::nt(LK) / 256) void k_mergek(
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
