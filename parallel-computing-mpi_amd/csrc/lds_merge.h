@@ -256,79 +256,6 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     }
 }
 
-// merge4 mirrored: the four keys of two DESCENDING pairs (v0 >= v1, n0 >= n1)
-// in descending order (max, max3, med3, min).
-[[maybe_unused]] __device__ __forceinline__ void merge4d(uint32_t v0, uint32_t v1, uint32_t n0, uint32_t n1, uint32_t& s0,
-                                                        uint32_t& s1, uint32_t& s2, uint32_t& s3) {
-    s0 = max(v0, n0);
-    const uint32_t a = min(v0, n0);
-    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(s1) : "v"(a), "v"(v1), "v"(n1));
-    s2 = max(min(a, v1), min(max(a, v1), n1));  // v_med3_u32
-    s3 = min(v1, n1);
-}
-[[maybe_unused]] __device__ __forceinline__ void merge4d(uint64_t v0, uint64_t v1, uint64_t n0, uint64_t n1, uint64_t& s0,
-                                                        uint64_t& s1, uint64_t& s2, uint64_t& s3) {
-    const bool c0 = v0 > n0, c1 = v1 > n1;
-    s0 = c0 ? v0 : n0;
-    const uint64_t a = c0 ? n0 : v0, m = c1 ? v1 : n1;
-    s3 = c1 ? n1 : v1;
-    const bool c2 = a > m;
-    s1 = c2 ? a : m;
-    s2 = c2 ? m : a;
-}
-
-// Bidirectional chains (MISORT_MK_BI): from ONE merge-path split (ia, ib) of
-// merge(s[A0..], s[B0..]) -- diagonal d = ia + ib -- the IH outputs below it
-// (d - IH .. d - 1) and the IH outputs above it (d .. d + IH - 1), as two
-// independent two-key chains interleaved step by step: r[0, IH) ascending
-// below, r[IH, 2 IH) above.  The upward chain is merge_chain_blk's; the
-// downward one is its mirror (it holds the two SMALLEST keys read and not yet
-// output, u0 >= u1; u1, the smallest key read, is the last read from side L,
-// every unread key of L lies below it; a step reads the next two keys below
-// from the other side S and outputs the highest two of the four).  A lane so
-// spends one co-rank search per 2 IH outputs instead of one per IH, and the
-// two chains give the lane two independent LDS reads in flight.  Each
-// sequence has >= IH + 2 words of MAX above it and >= IH zero words below it,
-// so neither chain checks an end.
-template <typename KEY, int ID, int IU, bool WIDE>
-__device__ __forceinline__ void merge_chain_bi(const KEY* s, int A0, int B0, int ia, int ib, KEY (&r)[ID + IU]) {
-    static_assert(ID % 2 == 0 && IU % 2 == 0 && ID >= 2 && IU >= ID, "two outputs per step, both directions");
-    constexpr uint32_t B2 = 2 * sizeof(KEY);
-    const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + ib);
-    const kvec2<KEY> fa = lds_ld2<KEY, WIDE>(pa), fb = lds_ld2<KEY, WIDE>(pb);
-    const kvec2<KEY> ba = lds_ld2<KEY, WIDE>(pa - B2), bb = lds_ld2<KEY, WIDE>(pb - B2);
-    // up: S = the side whose last read (largest) key is the smaller
-    const bool fas = fa.y <= fb.y;
-    uint32_t fps = (fas ? pa : pb) + B2, fpl = (fas ? pb : pa) + B2;
-    // down: S = the side whose last read (smallest) key is the larger; the
-    // pointers address the lowest key read
-    const bool bas = ba.x >= bb.x;
-    uint32_t bps = (bas ? pa : pb) - B2, bpl = (bas ? pb : pa) - B2;
-    KEY v0, v1, u0, u1;
-    merge4(fa.x, fa.y, fb.x, fb.y, r[ID], r[ID + 1], v0, v1);
-    merge4d(ba.y, ba.x, bb.y, bb.x, r[ID - 1], r[ID - 2], u0, u1);
-#pragma unroll
-    for (int k = 1; k < IU / 2; ++k) {
-        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(fps);
-        kvec2<KEY> m;
-        if (k < ID / 2) m = lds_ld2<KEY, WIDE>(bps - B2);
-        fps += B2;
-        const bool fsw = n.y > v1;
-        merge4(v0, v1, n.x, n.y, r[ID + 2 * k], r[ID + 2 * k + 1], v0, v1);
-        const uint32_t ft = fsw ? fpl : fps;
-        fpl = fsw ? fps : fpl;
-        fps = ft;
-        if (k < ID / 2) {
-            bps -= B2;
-            const bool bsw = m.x < u1;
-            merge4d(u0, u1, m.y, m.x, r[ID - 1 - 2 * k], r[ID - 2 - 2 * k], u0, u1);
-            const uint32_t bt = bsw ? bpl : bps;
-            bpl = bsw ? bps : bpl;
-            bps = bt;
-        }
-    }
-}
-
 // merge_chain_blk with ALIGNED two-key reads (chain 3: one ds_read_b64 for u32,
 // ds_read_b128 for u64, at the pair's own alignment -- the unaligned forms
 // measured 2.2x slower).  Every sequence starts at an even LDS slot, and the
@@ -614,109 +541,6 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                 st[p] = qp[p];
                 ln[p] = lp[p];
             }
-        }
-    }
-}
-
-// The in-LDS levels with bidirectional chains (merge_chain_bi): the first
-// S::NTM lanes merge (whole waves; the others only write sentinels), lane tid
-// owns outputs [tid * IT, tid * IT + IT) of a level and searches ONE co-rank,
-// at the middle of that range.  Layout: every sequence has GZ zero words below
-// it and G MAX words above it (S::G >= IT / 2 + 2, S::GZ >= IT / 2); a level's
-// pair outputs start at multiples of QA = IT past the previous pair's MAX and
-// zero words.  A lane whose middle diagonal d lies past its pair's end (tot
-// keys) splits at the even diagonal dc = tot or tot + 1 of the sequences
-// extended by their MAX words and writes [dc - IT/2, dc + IT/2): true outputs
-// of its neighbours' positions, MAX above the end and zeros below the pair's
-// start (the values those words hold anyway), so its stores stay even-aligned
-// pairs.  The last level's outputs stay in registers: r[0, IT) are positions
-// [tid * IT - ex, tid * IT - ex + IT) of the merged sequence.
-template <typename KEY, typename S>
-__device__ __forceinline__ void lds_merge_levels_bi(KEY* s, int (&st)[S::K], int (&ln)[S::K], KEY (&r)[S::IT], int& ex,
-                                                    int tid) {
-    constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, GZ = S::GZ, QA = S::QA;
-    // outputs below / above the lane's split: IT = 2 mod 4 splits unevenly (IT / 2
-    // odd keeps the lanes' splits and pair stores on distinct banks)
-    constexpr int ID = IT % 4 ? IT / 2 - 1 : IT / 2, IU = IT - ID;
-    static_assert(G >= IU + 2 && GZ >= ID && QA == IT && ID % 2 == 0 && IU % 2 == 0, "bidirectional layout");
-    constexpr bool WIDE = S::CH == 2;
-    constexpr KEY MAXK = KMAX<KEY>;
-    ex = 0;
-    const int pos = tid * IT;
-    const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
-#pragma unroll
-    for (int lv = 1; lv <= LK; ++lv) {
-        const int P = K >> lv;
-        int qp[K / 2], lp[K / 2];
-        int maxr = 0;
-        {
-            int qa = 0;
-#pragma unroll
-            for (int p = 0; p < K / 2; ++p) {
-                if (p >= P) break;
-                const int mr = ln[2 * p] < ln[2 * p + 1] ? ln[2 * p] : ln[2 * p + 1];
-                maxr = mr > maxr ? mr : maxr;
-                lp[p] = ln[2 * p] + ln[2 * p + 1];
-                qp[p] = qa;
-                qa = (qa + lp[p] + G + GZ + QA - 1) / QA * QA;
-            }
-        }
-        maxr = __builtin_amdgcn_readfirstlane(maxr);
-        int A0 = st[0], LA = ln[0], B0 = st[1], LB = ln[1], Q = 0, LP = lp[0];
-#pragma unroll
-        for (int p = 1; p < K / 2; ++p) {
-            if (p >= P) break;
-            const bool in = pos >= qp[p];
-            A0 = in ? st[2 * p] : A0;
-            LA = in ? ln[2 * p] : LA;
-            B0 = in ? st[2 * p + 1] : B0;
-            LB = in ? ln[2 * p + 1] : LB;
-            Q = in ? qp[p] : Q;
-            LP = in ? lp[p] : LP;
-        }
-        const int end = qp[P - 1] + lp[P - 1];
-        int base = pos;
-        if (wpos < end) {
-            const int d = pos + ID - Q, tot = LA + LB;
-            int dc = d < tot ? d : tot;
-            int ia = co_rank<KEY, S::MAXR, true>(s, A0, LA, B0, LB, dc, maxr);
-            if (d >= tot) {
-                const int od = tot & 1;
-                dc = tot + od;
-                ia = LA + od;
-            }
-            merge_chain_bi<KEY, ID, IU, WIDE>(s, A0, B0, ia, dc - ia, r);
-            base = Q + dc - ID;
-        }
-        lds_barrier();
-        if (lv < LK) {
-            if (pos < Q + LP) {
-#pragma unroll
-                for (int j = 0; j < IT; j += 2)
-                    *reinterpret_cast<kvec2<KEY>*>(s + base + j) = kvec2<KEY>{r[j], r[j + 1]};
-            }
-            // per pair: G MAX words above its output, GZ zero words below it
-            for (int x = tid; x < P * (G + GZ); x += NT) {
-                const int p = x / (G + GZ), w = x - p * (G + GZ);
-                int q0 = 0, e = 0;
-#pragma unroll
-                for (int q = 0; q < K / 2; ++q)
-                    if (q < P && p == q) {
-                        q0 = qp[q];
-                        e = qp[q] + lp[q];
-                    }
-                if (w < G) s[e + w] = MAXK;
-                else s[q0 - GZ + (w - G)] = (KEY)0;
-            }
-            lds_barrier();
-#pragma unroll
-            for (int p = 0; p < K / 2; ++p) {
-                if (p >= P) break;
-                st[p] = qp[p];
-                ln[p] = lp[p];
-            }
-        } else {
-            ex = pos - base;
         }
     }
 }

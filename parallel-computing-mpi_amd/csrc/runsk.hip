@@ -95,18 +95,11 @@ struct KTr;
 #endif
 // k_bounds loads the scanned fence counts beside the chunk-start fence (one
 // dependent round less) and divides chunk indices in 32 bits: 2^30 pass -2 to
-// -8 us, 2^28 and u64 equal (profiles/r05/plan/bearly_ab.txt); 0 = before
-#ifndef MISORT_BOUNDS_EARLY
-#define MISORT_BOUNDS_EARLY 1
-#endif
+// -8 us, 2^28 and u64 equal (profiles/r05/plan/bearly_ab.txt).
 constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 // u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
 // VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
 // (profiles/r03/ab1); 0 = loads into registers, then ds_write.
-// k_mergek chunks in one contiguous range per XCD (1) or chunk = block (0).
-#ifndef MISORT_MK_XCD
-#define MISORT_MK_XCD 0
-#endif
 #ifndef MISORT_MK_ZW
 #define MISORT_MK_ZW 1
 #endif
@@ -164,24 +157,6 @@ constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
 #ifndef MISORT_MK_RW16
 #define MISORT_MK_RW16 128
 #endif
-// 16-way u32 passes with bidirectional merge levels (lds_merge_levels_bi):
-// half the workgroup's lanes merge, each IT = MISORT_MK_BI_IT outputs per
-// level from ONE co-rank search at the middle of its range (a chain down and
-// a chain up, interleaved), so a chunk costs half the co-rank searches.
-#ifndef MISORT_MK_BI
-#define MISORT_MK_BI 0
-#endif
-#ifndef MISORT_MK_BI_IT
-#define MISORT_MK_BI_IT 26
-#endif
-#ifndef MISORT_MK_BI_NTM
-#define MISORT_MK_BI_NTM 512  // lanes that merge (whole waves)
-#endif
-// the largest chunk the bidirectional level layout holds (CAP + (K/2)(G + GZ +
-// QA) <= NT/2 * IT with G = IT/2 + 2, GZ = IT/2, QA = IT), or the override
-#ifndef MISORT_MK_CAPBI
-#define MISORT_MK_CAPBI 0
-#endif
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
@@ -194,16 +169,11 @@ struct KTr<uint32_t> {
     // the chunk shape of a pass of lk levels
     static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
     static constexpr int nt(int) { return NT; }
-    static constexpr bool bi(int lk) { return big(lk) && MISORT_MK_BI; }
-    static constexpr int cap_bi() {
-        return MISORT_MK_CAPBI ? MISORT_MK_CAPBI
-                               : MISORT_MK_BI_NTM * MISORT_MK_BI_IT - 8 * (2 * MISORT_MK_BI_IT + 4);
-    }
-    static constexpr int it(int lk) { return bi(lk) ? MISORT_MK_BI_IT : big(lk) ? MISORT_MK_IT16 : IT; }
+    static constexpr int it(int lk) { return big(lk) ? MISORT_MK_IT16 : IT; }
     // (k_fence_counts keeps 8-bit per-chunk counts: at most 255 + K fences of FG
     // keys a chunk, a bound only the 64-key build can reach)
     static constexpr int cap16() { return MISORT_MK_CAP16 < (255 + 16) * FG ? MISORT_MK_CAP16 : (255 + 16) * (int)FG; }
-    static constexpr int cap(int lk) { return bi(lk) ? cap_bi() : big(lk) ? cap16() : CAP; }
+    static constexpr int cap(int lk) { return big(lk) ? cap16() : CAP; }
     static constexpr int wg(int lk) { return big(lk) ? MISORT_MK_WGCU16 : WG_PER_CU; }
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = SORT_LT_MERGE, LWK_MAX = 30;  // runs >= the smaller SORT tile; 32-bit row offsets
@@ -234,7 +204,6 @@ struct KTr<uint64_t> {
     static constexpr int WG_PER_CU = MISORT_MK_WGCU64;
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
-    static constexpr bool bi(int) { return false; }
     static constexpr int nt(int) { return NT; }
     static constexpr int it(int) { return IT; }
     static constexpr int cap(int) { return CAP; }
@@ -256,9 +225,6 @@ struct Shape {
     // after each sequence: G >= the keys a chain may read past its sequence
     static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
     static constexpr int NT = T::nt(LK), IT = T::it(LK), CAP = T::cap(LK);
-    static constexpr bool BI = T::bi(LK);  // bidirectional levels (lds_merge_levels_bi)
-    static constexpr int NTM = BI ? MISORT_MK_BI_NTM : NT;  // lanes that merge
-    static_assert(NTM % 64 == 0 && NTM <= NT, "merging lanes: whole waves");
     static constexpr int MAXR = CAP / 2;  // co-rank range bound: min(LA, LB) <= CAP / 2
     // chain 3 merges RN = IT + 2 keys rounded up to even (the lane's IT outputs
     // after up to two early keys) and reads up to RN + 2 - 2 keys past a
@@ -269,20 +235,14 @@ struct Shape {
     // one's, so G exceeds the keys a chain reads past a sequence (IT for the
     // two-key chains, IT + 1 for the one-key chain)
     static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2 || (CH == 0 && MISORT_MK_ZW_CH0));
-    // BI: a lane's outputs below / above its split (lds_merge_levels_bi)
-    static constexpr int BID = IT % 4 ? IT / 2 - 1 : IT / 2, BIU = IT - BID;
-    static constexpr int G = BI ? BIU + 2 : CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
-    static constexpr int GZ = BI ? BID : 0;  // BI: zero words below every sequence
+    static constexpr int G = CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
     // level outputs start at lane boundaries; chain 3 also needs even slots
     static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
-    static_assert(!BI || (CH == 1 || CH == 2), "bidirectional levels: two-key chains");
     static_assert(CH != 3 || QA % 2 == 0, "chain 3: even sequence starts");
     static_assert(CH == 3 || IT % 2 == 0, "chains 0-2: outputs stored as aligned pairs");
     // LDS slot of segment q (o = its first chunk position): chain 3 reads
     // aligned pairs, so every sequence starts at an even slot
-    __device__ __host__ static int seg(int o, int q) {
-        return BI ? o + q * (G + GZ) : CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G;
-    }
+    __device__ __host__ static int seg(int o, int q) { return CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G; }
     static constexpr int K = 1 << LK, LKS = LK;
     static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
     static constexpr int RW = LK == 4 ? MISORT_MK_RW16 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
@@ -290,25 +250,20 @@ struct Shape {
     // load slots per lane: enough rows for CAP keys in K segments (18 at
     // CAP = 8192, IT = 17 or 18)
     static constexpr int LS_ROWS = ((CAP + RW - 1) / RW + K + NR - 1) / NR;
-    static constexpr int LS = BI || ((IT + 1) & ~1) <= LS_ROWS ? LS_ROWS : ((IT + 1) & ~1);
+    static constexpr int LS = ((IT + 1) & ~1) <= LS_ROWS ? LS_ROWS : ((IT + 1) & ~1);
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
-    // keys below s (a co-rank probe may read index -1; BI: the zero words
-    // below the first sequence), a multiple of 4 keeps s 16-byte aligned
-    static constexpr int PADK = BI ? (GZ + 3) / 4 * 4 : PAD;
-    static constexpr int BI_EXT = CAP + K * (G + GZ) > NTM * IT + G ? CAP + K * (G + GZ) : NTM * IT + G;
+    static constexpr int PADK = PAD;  // keys below s (a co-rank probe may read index -1)
     // the tile holds the chunk's segments with their sentinels (CAP + K G) and
     // every level's outputs (<= NT IT slots by the level layout, + G sentinels)
     static constexpr int NB_EXT = CAP + K * G > NT * IT + G ? CAP + K * G : NT * IT + G;
-    static constexpr int LDS_KEYS = BI ? PADK + BI_EXT + 16 : CH == 3 ? PAD + CAP + K * (G + QA) + 16 : PAD + NB_EXT + 16;
+    static constexpr int LDS_KEYS = CH == 3 ? PAD + CAP + K * (G + QA) + 16 : PAD + NB_EXT + 16;
     // the levels' pair table in LDS (MISORT_MK_PT)
     static constexpr bool PT = MISORT_MK_PT && K > 2;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
-    static_assert(BI ? CAP + (K / 2) * (G + GZ + QA) <= NTM * IT : CAP + (K / 2) * (G + QA) <= NT * IT,
-                  "level layout: pairs at lane boundaries");
+    static_assert(CAP + (K / 2) * (G + QA) <= NT * IT, "level layout: pairs at lane boundaries");
     static_assert(LDS_KEYS < 65536, "LDS key index of a row fits 16 bits");
-    static_assert(!BI || G + GZ <= 64, "sentinels: one wave per segment");
 };
 
 // fence <-> (key, tag): tag = run << (32 - lk) | position / FG, the low 32 bits
@@ -347,26 +302,47 @@ struct Geo {
         const int64_t glen = (n - base(g)) < K() * W() ? n - base(g) : K() * W();
         return (glen + FG - 1) >> FG_LOG2;
     }
-#if MISORT_BOUNDS_EARLY
     // a group's fences and chunks are < 2^31: a 32-bit division
     __device__ __host__ int64_t nchunks(int64_t g) const {
         return g < nfull ? kf : (int64_t)((uint32_t)(nfences(g) + fm - 1) / (uint32_t)fm);
     }
-#else
-    __device__ __host__ int64_t nchunks(int64_t g) const { return (nfences(g) + fm - 1) / fm; }
-#endif
     // bounds slot of chunk t of group g (each group has nchunks + 1 slots)
     __device__ __host__ int64_t slot(int64_t g, int64_t t) const {
         return g < nfull ? g * (kf + 1) + t : nfull * (kf + 1) + t;
     }
 };
 
+// fm = 0: the worst-case bound, (fm + K) * FG <= CAP
 template <typename KEY>
-Geo make_geo(int64_t n, int lw, int lk) {
-    Geo geo{n, lw, lk, KTr<KEY>::cap(lk) / (int)FG - (1 << lk), 0, 0};
+Geo make_geo(int64_t n, int lw, int lk, int fm = 0) {
+    Geo geo{n, lw, lk, fm > 0 ? fm : KTr<KEY>::cap(lk) / (int)FG - (1 << lk), 0, 0};
     geo.nfull = n >> (lw + lk);
     geo.kf = ((((int64_t)1 << (lw + lk)) >> FG_LOG2) + geo.fm - 1) / geo.fm;
     return geo;
+}
+
+// The capacity split's fences per chunk above the worst-case bound (merge_pass).
+// A chunk's size is FM * FG plus 2K window offsets of up to FG each, which
+// nearly cancel on spread keys (sigma ~ FG sqrt(2K / 12), 1.6 FG at K = 16):
+// 9 fences more at K = 16 (4.6 sigma of headroom with 128-key fences) and 3 at
+// K = 8 (4.3 sigma) keep splits to about one per few 2^30 passes on spread
+// keys -- a split's serial latency (k_split_desc) and its halves' merge sit on
+// the pass's critical path, so rarer splits beat fuller chunks here: 12 fences
+// more (2.8 sigma, ~0.3 % of chunks) measured slower than none at 2^28
+// (profiles/r06/mergek/split_ab.txt).  (env MISORT_MK_FM_ADD: one value
+// for every unfused pass, 0 = off), clamped so a half chunk still fits --
+// ceil(fm / 2) + K fences of FG keys <= CAP -- and fm <= 255 (k_fence_counts'
+// 8-bit counts).
+template <typename KEY, int LK>
+int split_fm_add() {
+    static const int env = getenv("MISORT_MK_FM_ADD") ? atoi(getenv("MISORT_MK_FM_ADD")) : -1;
+    // u64: equal kernel time, +25 us of split overhead per 2^29 pass (split_ab.txt): off
+    const int want = env >= 0 ? env : sizeof(KEY) == 8 ? 0 : LK == 4 ? 9 : LK == 3 ? 3 : 0;
+    const int K = 1 << LK, cap = KTr<KEY>::cap(LK), fm0 = cap / (int)FG - K;
+    int fm = fm0 + (want > 0 ? want : 0);
+    while (fm > fm0 && ((fm + 1) / 2 + K) * (int)FG > cap) --fm;
+    if (fm > 255) fm = 255;
+    return fm > fm0 ? fm - fm0 : 0;
 }
 
 // F[i] = fence of position i*FG (the first multi-way pass after the SORT tile).
@@ -544,7 +520,8 @@ constexpr int COUNT_NT = 1024, FC_NT = MISORT_FC_NT;
 static_assert(FC_NT >= SCAN_NT && FC_NT <= COUNT_NT && FC_NT % 64 == 0, "fence-count block");
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
-                                                           int cpb, int* __restrict__ P, int* __restrict__ bsum) {
+                                                           int cpb, int* __restrict__ P, int* __restrict__ bsum,
+                                                           int* __restrict__ ovf) {
     __shared__ uint64_t sws[COUNT_NT / 64];
 #if MISORT_FC_U32
     __shared__ uint32_t sc[SCAN_NT][16];
@@ -552,6 +529,7 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     __shared__ unsigned long long sc[SCAN_NT][2];
 #endif
     const int tid = threadIdx.x;
+    if (ovf && blockIdx.x == 0 && tid == 0) *ovf = 0;  // the capacity split's list, empty (k_chunk_desc fills it)
     const int64_t c0 = (int64_t)blockIdx.x * cpb, c = c0 + tid;  // cpb <= SCAN_NT chunks per block
     const int64_t c1 = c0 + cpb < nchunks ? c0 + cpb : nchunks;
     const int K = geo.K();
@@ -712,47 +690,22 @@ __device__ __forceinline__ int64_t interp(KEY v, KEY ka, KEY kb, int64_t a, int6
     }
 }
 
-// The start of chunk t of group g in run r (a position within the run), or
-// the run's length for the group's end slot (t = the group's chunk count).
-// Run r's fences before the chunk-start fence f come from the scanned counts;
-// the keys before f lie among the FG positions after the last of them.
+// Run r's position of the first key after fence f in the total order (key,
+// run, position) -- f's own position for r = f's run -- given lo = run r's
+// fences before f: the keys before f lie among the FG positions after the
+// last of them (-1: more fences than the run has, malformed input fences;
+// k_chunk_desc then rejects the chunk, no read outside the run).
 template <typename KEY>
-__device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
-                               const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
-                               const int* __restrict__ bsum, int cpb, const Geo& geo, int64_t g, int64_t t, int r,
-                               bool line) {
+__device__ int64_t window_bound(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                                const Geo& geo, int64_t g, int r, typename KTr<KEY>::F f, int64_t lo, bool line) {
     typedef typename KTr<KEY>::F FT;
     const int64_t base = geo.base(g), W = geo.W(), len = geo.run_len(g, r);
-    if (t == geo.nchunks(g)) return len;
-#if MISORT_BOUNDS_EARLY
-    // the scanned counts do not depend on the fence: their loads go out with
-    // the fence's (one dependent round less); chunk indices are < 2^31
-    const int K = geo.K();
-    const uint32_t c = (uint32_t)(g * geo.kf + t), c0 = (uint32_t)(g * geo.kf);  // the tail group starts at nfull * kf too
-    const int pc = P[(int64_t)c * K + r] + bsum[(int64_t)(c / (uint32_t)cpb) * K + r];
-    const int pc0 = P[(int64_t)c0 * K + r] + bsum[(int64_t)(c0 / (uint32_t)cpb) * K + r];
-    const FT f = M[(base >> FG_LOG2) + t * geo.fm];
-    const KEY v = (KEY)fkey(f);
-    const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (K - 1));
-    if (r == r0) return (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
-    if (len == 0) return 0;
-    const int64_t lo = (int64_t)pc - pc0;
-#else
-    const FT f = M[(base >> FG_LOG2) + t * geo.fm];
     const KEY v = (KEY)fkey(f);
     const int r0 = (int)((ftag(f) >> (32 - geo.lk)) & (geo.K() - 1));
     if (r == r0) return (int64_t)(ftag(f) & ((1u << (32 - geo.lk)) - 1)) << FG_LOG2;
     if (len == 0) return 0;
-    // fences of run r before f: counts of the group's chunks before chunk t
-    const int K = geo.K();
-    const int64_t c = g * geo.kf + t, c0 = g * geo.kf;  // the tail group starts at nfull * kf too
-    const int64_t lo = (int64_t)(P[c * K + r] + bsum[(c / cpb) * K + r]) -
-                       (P[c0 * K + r] + bsum[(c0 / cpb) * K + r]);
-#endif
     if (lo <= 0) return 0;  // run r's first key comes after f
-    if (lo > (len + FG - 1) >> FG_LOG2) return -1;  // more fences than the run has: malformed input
-                                                    // fences; k_chunk_desc rejects the chunk, no read
-                                                    // outside the run
+    if (lo > (len + FG - 1) >> FG_LOG2) return -1;
     // keys before f: all of positions <= (lo-1)*FG, none from lo*FG on.  The
     // first position after f (key > v if r < r0, key >= v if r > r0) lies in
     // [a, b]; it is guessed by interpolating v between the window's two
@@ -845,6 +798,25 @@ __device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<K
     return lo_b;
 }
 
+
+// The start of chunk t of group g in run r (a position within the run), or
+// the run's length for the group's end slot (t = the group's chunk count).
+// Run r's fences before the chunk-start fence f come from the scanned counts
+// (loaded beside f: one dependent round less; chunk indices are < 2^31).
+template <typename KEY>
+__device__ int64_t chunk_bound(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                               const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                               const int* __restrict__ bsum, int cpb, const Geo& geo, int64_t g, int64_t t, int r,
+                               bool line) {
+    if (t == geo.nchunks(g)) return geo.run_len(g, r);
+    const int K = geo.K();
+    const uint32_t c = (uint32_t)(g * geo.kf + t), c0 = (uint32_t)(g * geo.kf);  // the tail group starts at nfull * kf too
+    const int pc = P[(int64_t)c * K + r] + bsum[(int64_t)(c / (uint32_t)cpb) * K + r];
+    const int pc0 = P[(int64_t)c0 * K + r] + bsum[(int64_t)(c0 / (uint32_t)cpb) * K + r];
+    const typename KTr<KEY>::F f = M[(geo.base(g) >> FG_LOG2) + t * geo.fm];
+    return window_bound<KEY>(src, F, geo, g, r, f, (int64_t)pc - pc0, line);
+}
+
 // One thread per (bounds slot, run).
 template <typename KEY>
 __global__ void k_bounds(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
@@ -904,6 +876,111 @@ struct DescHdr {
     uint32_t sb[K];
 };
 
+// A chunk's descriptor header from its bounds st / en in the K runs of group g
+// (ok = false: an empty chunk): the segments' chunk positions, load-row
+// counts and byte offsets, the row -> segment map, and the output offset.
+template <typename KEY, int LK, bool UNROLL = true>
+__device__ void desc_header(DescHdr<KEY, LK>& h, uint8_t* seg, const Geo& geo, int64_t g, const int64_t* st,
+                            const int64_t* en, bool ok) {
+    typedef Shape<KEY, LK> S;
+    constexpr int K = S::K;
+    int R = 0, o = 0;
+    int64_t out = geo.base(g);
+#pragma unroll(UNROLL ? K : 1)
+    for (int r = 0; r < K; ++r) {
+        const int ln = ok ? (int)(en[r] - st[r]) : 0, s0 = ok ? (int)st[r] : 0;
+        h.srow[r] = R;
+        h.so[r] = o;
+        h.sln[r] = ln;
+        // byte offset of segment r's first key from the group base (< KW*sizeof(KEY) <= 2^32)
+        h.sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)s0) * (uint32_t)sizeof(KEY);
+        const int nr = (ln + S::RW - 1) / S::RW;
+        for (int q = 0; q < nr; ++q) seg[R + q] = (uint8_t)r;
+        R += nr;
+        o += ln;
+        out += s0;
+    }
+    h.srow[K] = R;
+    h.so[K] = o;
+    h.gbase = geo.base(g);
+    h.out0 = out;
+}
+
+// Table entry j of a descriptor from its header (entry j is row (j % LS) * NR
+// + j / LS: stored by part).
+template <typename KEY, int LK>
+__device__ __forceinline__ void desc_entry(Desc<KEY, LK>* d, const DescHdr<KEY, LK>& h, const uint8_t* seg, int j) {
+    typedef Shape<KEY, LK> S;
+    constexpr int K = S::K;
+    const int row = (j % S::LS) * S::NR + j / S::LS;
+    uint32_t off = 0, la = 0;
+    if (row < h.srow[K]) {  // rows past the chunk: no keys
+        const int rr = seg[row];
+        const int k = row - h.srow[rr], rem = h.sln[rr] - k * S::RW;
+        off = h.sb[rr] + (uint32_t)(k * S::RW * (int)sizeof(KEY));
+        la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(S::seg(h.so[rr], rr) + k * S::RW) << 16);
+    }
+    d->off[j] = off;
+    d->la[j] = la;
+}
+
+// The capacity split (merge_pass): chunk (g, t), whose exact size exceeds CAP,
+// cut at its middle merged fence into two descriptors d[0], d[1] by the 64
+// lanes of one wave.  Each half holds at most ceil(fm / 2) + K fences' worth
+// of keys <= CAP (merge_pass bounds fm so).  Lane r < K finds run r's bound at
+// the middle fence: its fences before the chunk start (the scanned counts)
+// plus those among the chunk's first fences, then the window search of
+// k_bounds; lanes 0 and 1 build the halves' headers.  hdr / seg / sm: LDS
+// scratch for two headers and K bounds.
+template <typename KEY, int LK>
+__device__ __forceinline__ void split_chunk(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                            const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                            const int* __restrict__ bsum, int cpb, const Geo& geo, int64_t g, int64_t t,
+                            const int64_t* b0, Desc<KEY, LK>* d, int* err, bool line, DescHdr<KEY, LK>* hdr,
+                            uint8_t (*seg)[Shape<KEY, LK>::NROWS], int64_t* sm, int lane) {
+    typedef Shape<KEY, LK> S;
+    constexpr int K = S::K, NROWS = S::NROWS;
+    const int64_t gf = geo.base(g) >> FG_LOG2, nfg = geo.nfences(g), f0 = t * geo.fm;
+    const int mid = (int)((f0 + geo.fm < nfg ? geo.fm : nfg - f0) / 2);
+    if (lane < K) {
+        const int r = lane;
+        const uint32_t c = (uint32_t)(g * geo.kf + t), c0 = (uint32_t)(g * geo.kf);
+        int64_t lo = (int64_t)(P[(int64_t)c * K + r] + bsum[(int64_t)(c / (uint32_t)cpb) * K + r]) -
+                     (P[(int64_t)c0 * K + r] + bsum[(int64_t)(c0 / (uint32_t)cpb) * K + r]);
+        for (int e = 0; e < mid; ++e) lo += (int)((ftag(M[gf + f0 + e]) >> (32 - geo.lk)) & (K - 1)) == r ? 1 : 0;
+        sm[r] = mid > 0 ? window_bound<KEY>(src, F, geo, g, r, M[gf + f0 + mid], lo, line) : -1;
+    }
+    __syncthreads();
+    if (lane < 2) {
+        // half 0: [b0, sm), half 1: [sm, b0 + K) (generic pointers: few registers)
+        const int64_t* st = lane ? sm : b0;
+        const int64_t* en = lane ? b0 + K : sm;
+        bool ok = mid > 0;
+        int64_t tot = 0;
+        for (int r = 0; r < K; ++r) {
+            ok = ok && st[r] >= 0 && en[r] >= st[r] && en[r] <= geo.run_len(g, r);
+            tot += en[r] - st[r];
+        }
+        ok = ok && tot <= S::CAP;
+        if (!ok) atomicOr(err, 1);
+        desc_header<KEY, LK, false>(hdr[lane], seg[lane], geo, g, st, en, ok);
+    }
+    __syncthreads();
+    for (int e = lane; e < 2 * NROWS; e += 64) {
+        const int h = e / NROWS;
+        desc_entry<KEY, LK>(d + h, hdr[h], seg[h], e - h * NROWS);
+    }
+    for (int e = lane; e < 2 * (K + 1); e += 64) {
+        const int h = e / (K + 1), r = e - h * (K + 1);
+        d[h].o[r] = hdr[h].so[r];
+    }
+    if (lane < 2) {
+        d[lane].gbase = hdr[lane].gbase;
+        d[lane].out0 = hdr[lane].out0;
+    }
+    __syncthreads();
+}
+
 // PLAN (small sorts, MISORT_PLAN_FUSE): the workgroup computes its chunks'
 // bounds itself (chunk_bound: the DC chunk starts and the end of the last one,
 // lane = (chunk, run)) into LDS, in place of a k_bounds launch.  nbs > 0: bsum
@@ -919,7 +996,8 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
                                                    const typename KTr<KEY>::F* __restrict__ M = nullptr,
                                                    const int* __restrict__ P = nullptr,
                                                    const int* __restrict__ bsum = nullptr, int cpb = 0,
-                                                   bool line = false, int nbs = 0) {
+                                                   bool line = false, int nbs = 0, int* __restrict__ ovf = nullptr,
+                                                   Desc<KEY, LK>* __restrict__ dov = nullptr) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NROWS = S::NROWS;
     __shared__ DescHdr<KEY, LK> hdr[DC];
@@ -994,48 +1072,22 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             const int64_t ln = en[r] - st[r];
-            ok = ok && st[r] >= 0 && ln >= 0 && en[r] <= geo.run_len(g, r) && ln <= S::CAP;
+            ok = ok && st[r] >= 0 && ln >= 0 && en[r] <= geo.run_len(g, r);
             tot += ln;
         }
-        ok = ok && tot <= S::CAP;
-        if (!ok) atomicOr(err, 1);  // a planning bug: the chunk stays unwritten, the host is told
-        DescHdr<KEY, LK>& h = hdr[lane];
-        int R = 0, o = 0;
-        int64_t out = geo.base(g);
-#pragma unroll
-        for (int r = 0; r < K; ++r) {
-            const int ln = ok ? (int)(en[r] - st[r]) : 0, s0 = ok ? (int)st[r] : 0;
-            h.srow[r] = R;
-            h.so[r] = o;
-            h.sln[r] = ln;
-            // byte offset of segment r's first key from the group base (< KW*sizeof(KEY) <= 2^32)
-            h.sb[r] = (((uint32_t)r << geo.lw) + (uint32_t)s0) * (uint32_t)sizeof(KEY);
-            const int nr = (ln + S::RW - 1) / S::RW;
-            for (int q = 0; q < nr; ++q) seg[lane][R + q] = (uint8_t)r;
-            R += nr;
-            o += ln;
-            out += s0;
-        }
-        h.srow[K] = R;
-        h.so[K] = o;
-        h.gbase = geo.base(g);
-        h.out0 = out;
+        // ovf (fm above the worst-case bound, see merge_pass): a chunk larger
+        // than CAP keys gets an empty descriptor here and is listed in ovf for
+        // k_split_desc
+        const bool big = ok && tot > S::CAP;
+        if (big && ovf) ovf[1 + atomicAdd(ovf, 1)] = (int)(cb + lane);
+        else if (!ok || big) atomicOr(err, 1);  // a planning bug: the chunk stays unwritten, the host is told
+        desc_header<KEY, LK>(hdr[lane], seg[lane], geo, g, st, en, ok && !big);
     }
     __syncthreads();
     Desc<KEY, LK>* d = desc + cb;
     for (int e = lane; e < nc * NROWS; e += DC_NT) {
-        const int cl = e / NROWS, j = e - cl * NROWS;
-        const DescHdr<KEY, LK>& h = hdr[cl];
-        const int row = (j % S::LS) * S::NR + j / S::LS;  // table entry j (stored by part)
-        uint32_t off = 0, la = 0;
-        if (row < h.srow[K]) {  // rows past the chunk: no keys
-            const int rr = seg[cl][row];
-            const int k = row - h.srow[rr], rem = h.sln[rr] - k * S::RW;
-            off = h.sb[rr] + (uint32_t)(k * S::RW * (int)sizeof(KEY));
-            la = (uint32_t)(rem < S::RW ? rem : S::RW) | ((uint32_t)(S::seg(h.so[rr], rr) + k * S::RW) << 16);
-        }
-        d[cl].off[j] = off;
-        d[cl].la[j] = la;
+        const int cl = e / NROWS;
+        desc_entry<KEY, LK>(d + cl, hdr[cl], seg[cl], e - cl * NROWS);
     }
     for (int e = lane; e < nc * (K + 1); e += DC_NT) {
         const int cl = e / (K + 1), r = e - cl * (K + 1);
@@ -1044,6 +1096,29 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
     if (lane < nc) {
         d[lane].gbase = hdr[lane].gbase;
         d[lane].out0 = hdr[lane].out0;
+    }
+}
+
+// The chunks k_chunk_desc listed (ovf[1 .. ovf[0]]), each cut in two into
+// dov[2i], dov[2i + 1] (split_chunk): one wave per listed chunk, a small grid
+// (the list is usually empty: it exits at once; long only for adversarial runs).
+constexpr int SPLIT_WG = 64;
+template <typename KEY, int LK>
+__global__ __launch_bounds__(64) void k_split_desc(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
+                                                  const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
+                                                  const int* __restrict__ bsum, int cpb, Geo geo,
+                                                  const int64_t* __restrict__ bounds, const int* __restrict__ ovf,
+                                                  Desc<KEY, LK>* __restrict__ dov, int* __restrict__ err, bool line) {
+    typedef Shape<KEY, LK> S;
+    __shared__ DescHdr<KEY, LK> hdr[2];
+    __shared__ uint8_t seg[2][S::NROWS];
+    __shared__ int64_t sm[S::K];
+    const int cnt = ovf[0];
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+        int64_t g, t;
+        chunk_place(geo, ovf[1 + i], g, t);
+        split_chunk<KEY, LK>(src, F, M, P, bsum, cpb, geo, g, t, bounds + S::K * geo.slot(g, t), dov + 2 * (int64_t)i,
+                             err, line, hdr, seg, sm, (int)threadIdx.x);
     }
 }
 
@@ -1095,8 +1170,7 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
         st[q] = S::seg(d->o[q], q);
         ln[q] = d->o[q + 1] - d->o[q];
     }
-    if constexpr (S::BI) lds_merge_levels_bi<KEY, S>(s, st, ln, r, ex, tid);
-    else lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
+    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
     const int64_t out0 = d->out0;
     // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
@@ -1109,9 +1183,6 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
             // 16-byte) write per two keys instead of one write per key
 #pragma unroll
             for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(q + j) = kvec2<KEY>{r[j], r[j + 1]};
-        } else if constexpr (S::BI) {
-#pragma unroll
-            for (int k = 0; k < IT; ++k) q[k] = r[k];
         } else {
 #pragma unroll
             for (int k = 0; k < RN; ++k)
@@ -1154,15 +1225,6 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
     // by scalar loads), G <= 64 lanes each
     static_assert(S::G <= 64, "sentinels: one wave per segment");
     const int lane = tid & 63;
-    if constexpr (S::BI) {
-        // G MAX words above each segment, GZ zero words below it
-        for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64) {
-            const int b = S::seg(d->o[q], q);
-            if (lane < S::G) s[b + (d->o[q + 1] - d->o[q]) + lane] = KMAX<KEY>;
-            else if (lane < S::G + S::GZ) s[b - S::GZ + (lane - S::G)] = (KEY)0;
-        }
-        return;
-    }
     for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64)
         if (lane < S::G)
             s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = S::ZW && lane == S::G - 1 ? (KEY)0 : KMAX<KEY>;
@@ -1187,25 +1249,14 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
 // attribution: 3 - 1 = the searches, 0 - 3 = the chains).
 // Waves whose lanes all lie past a level's outputs skip its merge (a chunk
 // averages FM*FG of CAP keys).
-template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
-__global__ __launch_bounds__(KTr<KEY>::nt(LK), KTr<KEY>::wg(LK)* KTr<KEY>::nt(LK) / 256) void k_mergek(
-    const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
-    typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn) {
+// One chunk: its rows into LDS, the sentinels, then mergek_chunk.
+template <typename KEY, int LK, bool FENCES, int MODE, bool ORD>
+__device__ __forceinline__ void mergek_run(KEY* tile, PairRec* pt, const KEY* __restrict__ src, KEY* __restrict__ dst,
+                                           const Desc<KEY, LK>* __restrict__ d, typename KTr<KEY>::F* __restrict__ fout,
+                                           int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
-    __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
-    __shared__ PairRec ptab[S::PT ? S::K / 2 : 1];
-    PairRec* pt = S::PT ? ptab : nullptr;
     KEY* s = tile + S::PADK;
     const int tid = threadIdx.x;
-    uint32_t chunk = blockIdx.x;
-    if constexpr (MISORT_MK_XCD) {
-        // blocks b, b + 8, ... share an XCD (round-robin dispatch): give each
-        // XCD one contiguous range of chunks, so neighbouring chunks' shared
-        // boundary lines meet in one L2 (a bijection for any grid size)
-        const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7, q = nb >> 3, rm = nb & 7;
-        chunk = x * q + (x < rm ? x : rm) + (b >> 3);
-    }
-    const Desc<KEY, LK>* d = desc + chunk;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
         // table entries first (scalar registers), then all its loads
@@ -1245,6 +1296,32 @@ __global__ __launch_bounds__(KTr<KEY>::nt(LK), KTr<KEY>::wg(LK)* KTr<KEY>::nt(LK
     }
     __syncthreads();
     mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid, pt);
+}
+
+// The grid: (capacity split) first OVF_WG workgroups that walk the halves of
+// the chunks k_split_desc cut (2 * ovf[0] descriptors in dov; usually none:
+// they exit at once; dispatched first, so a half never trails the pass), then
+// one workgroup per chunk.
+constexpr int OVF_WG = 256;
+template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
+__global__ __launch_bounds__(KTr<KEY>::nt(LK), KTr<KEY>::wg(LK)* KTr<KEY>::nt(LK) / 256) void k_mergek(
+    const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
+    typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, uint32_t nprimary,
+    const Desc<KEY, LK>* __restrict__ dov = nullptr, const int* __restrict__ ovf = nullptr) {
+    typedef Shape<KEY, LK> S;
+    __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
+    __shared__ PairRec ptab[S::PT ? S::K / 2 : 1];
+    const uint32_t nov = gridDim.x - nprimary;  // the split's workgroups (0 without it)
+    if (blockIdx.x >= nov) {
+        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, S::PT ? ptab : nullptr, src, dst, desc + (blockIdx.x - nov), fout,
+                                               lwn, lkn);
+        return;
+    }
+    const int cnt = 2 * ovf[0];
+    for (int i = (int)blockIdx.x; i < cnt; i += (int)nov) {
+        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, S::PT ? ptab : nullptr, src, dst, dov + i, fout, lwn, lkn);
+        __syncthreads();  // the tile is reused
+    }
 }
 
 // Fence buffers, bounds and descriptors: one grow-only set per (device, stream).
@@ -1321,7 +1398,24 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
                       int lk_next, LaunchHook* hook, bool ord_out, int depth = 0) {
     typedef Shape<KEY, LK> S;
     typedef typename KTr<KEY>::F FT;
-    const Geo geo = make_geo<KEY>(n, lw, LK);
+    // MISORT_PLAN_FUSE: 1 (default) = bounds inside k_chunk_desc below 4096
+    // chunks, 2 = at every size, 0 = never (profiles/r03/ab_plan: 2^24 u32 43.1
+    // -> 43.9 Gkeys/s; at 2^26, 9362 chunks, 65.2 -> 65.0)
+    // MISORT_PLAN_SCAN: 1 (default) = a fused descriptor kernel scans the
+    // fence-count block totals itself when they fit PLAN_SCAN_MAX, 0 = never
+    static const int plan_fuse = getenv("MISORT_PLAN_FUSE") ? atoi(getenv("MISORT_PLAN_FUSE")) : 1;
+    static const int plan_scan = getenv("MISORT_PLAN_SCAN") ? atoi(getenv("MISORT_PLAN_SCAN")) : 1;
+    Geo geo = make_geo<KEY>(n, lw, LK);
+    const bool fuse = plan_fuse == 2 || (plan_fuse == 1 && chunks_of(geo) < 4096);
+    // Capacity split (unfused passes): chunks cut every fm merged fences, fm
+    // above the worst-case bound by split_fm_add -- sized for a typical chunk,
+    // whose K window offsets nearly cancel -- and the rare chunk that exceeds
+    // CAP cut in two at its middle fence (k_chunk_desc cuts it, k_mergek's
+    // extra workgroups run the halves).  A half holds at most ceil(fm / 2) + K fences'
+    // worth of keys, so fm stays within 2 (CAP / FG - K) (and 8-bit counts).
+    const int fma = fuse ? 0 : split_fm_add<KEY, LK>();
+    if (fma > 0) geo = make_geo<KEY>(n, lw, LK, geo.fm + fma);
+    const bool split = fma > 0;
     const bool tail = (geo.nfull << (lw + LK)) < n;
     const int64_t nchunks = chunks_of(geo);
     const int64_t nslots = geo.nfull * (geo.kf + 1) + (tail ? geo.nchunks(geo.nfull) + 1 : 0);
@@ -1339,7 +1433,11 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     const size_t cb = ((size_t)nbk * cpb * S::K * 4 + 255) & ~(size_t)255;
     const size_t sb = ((size_t)nbk * S::K * 4 + 255) & ~(size_t)255;
     char* fbase = (char*)scratch(2 * depth, 2 * fb, s);
-    char* base = (char*)scratch(2 * depth + 1, 2 * fb + bb + cb + sb + (size_t)nchunks * sizeof(Desc<KEY, LK>) + 256, s);
+    // descriptors: one per chunk, and with the split two per listed chunk
+    // (at most every chunk) plus the list
+    const size_t db = (size_t)nchunks * sizeof(Desc<KEY, LK>) * (split ? 3 : 1);
+    const size_t ob = split ? ((size_t)(nchunks + 1) * 4 + 255) & ~(size_t)255 : 0;
+    char* base = (char*)scratch(2 * depth + 1, 2 * fb + bb + cb + sb + db + ob + 256, s);
     int* ew = error_word(s);
     if (!base || !fbase || !ew) return hipErrorOutOfMemory;
     FT* F = (FT*)(fbase + (phase & 1) * fb);
@@ -1350,6 +1448,8 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     int* cnt = (int*)(base + 2 * fb + bb);
     int* bsum = (int*)(base + 2 * fb + bb + cb);
     Desc<KEY, LK>* desc = (Desc<KEY, LK>*)(base + 2 * fb + bb + cb + sb);
+    Desc<KEY, LK>* dov = split ? desc + nchunks : nullptr;  // the halves of listed chunks
+    int* ovf = split ? (int*)(base + 2 * fb + bb + cb + sb + db) : nullptr;  // [count, chunks...]
     if (gather) k_fence_gather<KEY><<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
     const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
     {
@@ -1407,20 +1507,12 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
     // MISORT_FC_SLICES_MAX (tests): the block count from which the coalesced form counts
     static const int64_t slices_max = getenv("MISORT_FC_SLICES_MAX") ? atoll(getenv("MISORT_FC_SLICES_MAX")) : 256;
-    if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
-    else k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum);
+    if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
+    else k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
     // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
     static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
     static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
-    // MISORT_PLAN_FUSE: 1 (default) = bounds inside k_chunk_desc below 4096
-    // chunks, 2 = at every size, 0 = never (profiles/r03/ab_plan: 2^24 u32 43.1
-    // -> 43.9 Gkeys/s; at 2^26, 9362 chunks, 65.2 -> 65.0)
-    // MISORT_PLAN_SCAN: 1 (default) = a fused descriptor kernel scans the
-    // fence-count block totals itself when they fit PLAN_SCAN_MAX, 0 = never
-    static const int plan_fuse = getenv("MISORT_PLAN_FUSE") ? atoi(getenv("MISORT_PLAN_FUSE")) : 1;
-    static const int plan_scan = getenv("MISORT_PLAN_SCAN") ? atoi(getenv("MISORT_PLAN_SCAN")) : 1;
     const bool line = (nslots << LK) >= line_min;
-    const bool fuse = plan_fuse == 2 || (plan_fuse == 1 && nchunks < 4096);
     const int nbs = fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
     if (nbs == 0) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
     if (!fuse)
@@ -1429,28 +1521,39 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // the launch before k_mergek: a binding hook's tick (its end starts k_mergek's record)
     hipEvent_t ta = nullptr, tb = nullptr;
     if (hook && hook->binds()) (void)hook->bind(-1, -1, 0.0, &ta, &tb);
+    hipEvent_t da = ta, dbe = tb;
     const dim3 g16((unsigned)((nchunks + 15) / 16)), g4((unsigned)((nchunks + 3) / 4));
     const int* P0 = cnt;
     const FT* F0 = F;
     const FT* M0 = M;
     if (fuse) {
         if (nchunks >= dc16_min)
-            launch_timed(k_chunk_desc<KEY, LK, 16, true>, g16, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)nullptr, geo,
-                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs);
+            launch_timed(k_chunk_desc<KEY, LK, 16, true>, g16, dim3(DC_NT), 0, s, da, dbe, (const int64_t*)nullptr, geo,
+                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs, (int*)nullptr,
+                         (Desc<KEY, LK>*)nullptr);
         else
-            launch_timed(k_chunk_desc<KEY, LK, 4, true>, g4, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)nullptr, geo,
-                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs);
+            launch_timed(k_chunk_desc<KEY, LK, 4, true>, g4, dim3(DC_NT), 0, s, da, dbe, (const int64_t*)nullptr, geo,
+                         nchunks, desc, ew, src, F0, M0, P0, (const int*)bsum, cpb, line, nbs, (int*)nullptr,
+                         (Desc<KEY, LK>*)nullptr);
     } else {
         if (nchunks >= dc16_min)
-            launch_timed(k_chunk_desc<KEY, LK, 16, false>, g16, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)bounds,
+            launch_timed(k_chunk_desc<KEY, LK, 16, false>, g16, dim3(DC_NT), 0, s, da, dbe, (const int64_t*)bounds,
                          geo, nchunks, desc, ew, (const KEY*)nullptr, (const FT*)nullptr, (const FT*)nullptr,
-                         (const int*)nullptr, (const int*)nullptr, 0, false, 0);
+                         (const int*)nullptr, (const int*)nullptr, 0, false, 0, ovf, (Desc<KEY, LK>*)nullptr);
         else
-            launch_timed(k_chunk_desc<KEY, LK, 4, false>, g4, dim3(DC_NT), 0, s, ta, tb, (const int64_t*)bounds, geo,
+            launch_timed(k_chunk_desc<KEY, LK, 4, false>, g4, dim3(DC_NT), 0, s, da, dbe, (const int64_t*)bounds, geo,
                          nchunks, desc, ew, (const KEY*)nullptr, (const FT*)nullptr, (const FT*)nullptr,
-                         (const int*)nullptr, (const int*)nullptr, 0, false, 0);
+                         (const int*)nullptr, (const int*)nullptr, 0, false, 0, ovf, (Desc<KEY, LK>*)nullptr);
     }
-    const unsigned grid = (unsigned)nchunks;
+    // the listed chunks' halves (k_mergek's extra workgroups merge them)
+    if (split)
+        k_split_desc<KEY, LK><<<SPLIT_WG, 64, 0, s>>>(src, F0, M0, P0, (const int*)bsum, cpb, geo,
+                                                      (const int64_t*)bounds, ovf, dov, ew, line);
+    // the capacity split: OVF_WG more workgroups walk the cut chunks' halves
+    const unsigned grid = (unsigned)nchunks + (split ? OVF_WG : 0);
+    const uint32_t np = (uint32_t)nchunks;
+    const Desc<KEY, LK>* dv = dov;
+    const int* ov = ovf;
     // a binding hook: the launch carries its own events and ends the pass's
     // record; else marker events around it (nested in the pass's)
     const double kb = 2.0 * (double)n * sizeof(KEY);
@@ -1460,14 +1563,14 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     else if (hook) hook->before(KIND_RUNSK_KERNEL, kb, s);
     if (lk_next > 0) {
         launch_timed(k_mergek<KEY, LK, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
-                     (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next);
+                     (const Desc<KEY, LK>*)desc, Fn, lw + LK, lk_next, np, dv, ov);
     } else if (ord_out) {
         if constexpr (sizeof(KEY) == 8)
             launch_timed(k_mergek<KEY, LK, false, 0, true>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
-                         (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
+                         (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0, np, dv, ov);
     } else {
         launch_timed(k_mergek<KEY, LK, false>, dim3(grid), dim3(S::NT), 0, s, ea, eb, src, dst,
-                     (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0);
+                     (const Desc<KEY, LK>*)desc, (FT*)nullptr, 0, 0, np, dv, ov);
     }
     if (hook && !bound) hook->after(KIND_RUNSK_KERNEL, s);
     static const bool probe = getenv("MISORT_MK_PROBE") && atoi(getenv("MISORT_MK_PROBE")) != 0;
@@ -1481,9 +1584,9 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             if (hipMalloc(&junk, (size_t)n * sizeof(KEY)) != hipSuccess) return hipErrorOutOfMemory;
             junk_n = (size_t)n;
         }
-        k_mergek<KEY, LK, false, 1><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
-        k_mergek<KEY, LK, false, 2><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
-        k_mergek<KEY, LK, false, 3><<<grid, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0);
+        k_mergek<KEY, LK, false, 1><<<np, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0, np, dv, ov);
+        k_mergek<KEY, LK, false, 2><<<np, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0, np, dv, ov);
+        k_mergek<KEY, LK, false, 3><<<np, S::NT, 0, s>>>(src, junk, desc, nullptr, 0, 0, np, dv, ov);
     }
     return hipGetLastError();
 }

@@ -175,6 +175,7 @@ else:
 out = torch.empty_like(d)
 ctx.parallel_bitonic_sort(d, n, n, out=out)
 ctx.local_sort(d)  # in place (ping-pong through the context's scratch)
+ctx.synchronize()  # raises MISORT_E_INTERNAL if a merge pass rejected a chunk
 torch.cuda.synchronize()
 iv = torch.int32 if kb == 4 else torch.int64
 a = out.view(iv).cpu().numpy().view(dt)
@@ -228,6 +229,17 @@ ctx.close()
     (4, {"MISORT_FENCE_FG6_MIN": "20", "MISORT_MULTIWAY": "3"}, (1 << 24) + 12345),
     (8, {"MISORT_FENCE_FG6_MIN_U64": "20"}, (1 << 25) + 12345),
     (8, {"MISORT_FENCE_FG6_MIN_U64": "20"}, (1 << 22) + 3),
+    # the capacity split (merge_pass): far more fences per chunk than the
+    # defaults, so most chunks exceed CAP and run as two halves
+    # (k_split_desc, k_mergek_ovf); u32 16-way, 8-way, 64-key fences, nested
+    # fence passes, u64
+    (4, {"MISORT_MK_FM_ADD": "80"}, (1 << 26) + 12345),
+    (4, {"MISORT_MK_FM_ADD": "84"}, (1 << 27) + 777),
+    (4, {"MISORT_MK_FM_ADD": "30", "MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),
+    (4, {"MISORT_MK_FM_ADD": "40", "MISORT_FENCE_FG6_MIN": "20"}, (1 << 26) + 12345),
+    (4, {"MISORT_MK_FM_ADD": "60", "MISORT_FENCE_NEST_MIN": "12"}, (1 << 27) + 777),
+    (4, {"MISORT_MK_FM_ADD": "0"}, (1 << 26) + 777),  # no split: the worst-case chunk bound
+    (8, {"MISORT_MK_FM_ADD": "40"}, (1 << 25) + 12345),
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),
     (8, {"MISORT_RUN_NT": "512"}, (1 << 20) + 5),
