@@ -101,16 +101,11 @@ struct KT<uint64_t> {
 
 
 // u64 compare-exchanges on one v_cmp_u64 (cx); register stages batch their
-// compares ahead of the selects (reg_stages_c).
-#ifndef MISORT_CX64_ONECMP
-#define MISORT_CX64_ONECMP 1
-#endif
-#ifndef MISORT_CX64_BATCH
-#define MISORT_CX64_BATCH 1
-#endif
+// compares ahead of the selects (reg_stages_c): u64 SORT tile at 2^29 6.71 ->
+// 5.78 ms (one compare, profiles/r03/ab2) -> 5.58 ms (batched, profiles/r03/ab4).
 template <typename K>
 __device__ __forceinline__ void cx(K& a, K& b) {
-    if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP) {
+    if constexpr (sizeof(K) == 8) {
         // no 64-bit min/max: as min and max each would cost a v_cmp_u64 + 2
         // v_cndmask, the selects take one compare -- the empty asm hides that
         // the selected values are the compared ones, so they are not folded
@@ -244,7 +239,7 @@ __device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
 #pragma unroll
     for (int r = TOP; r > TOP - CNT; --r) {
         const bool fl = FLIP && r == TOP;
-        if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP && MISORT_CX64_BATCH) {
+        if constexpr (sizeof(K) == 8) {
             // u64: the stage's 16 compares first, then the selects (cx<u64>
             // one pair at a time waits 2 cycles between each compare and its
             // selects)
@@ -276,17 +271,15 @@ __device__ __forceinline__ void reg_stages_c(K (&v)[32]) {
 }
 
 // Levels 1..5 of the tile: the 32 register keys of a lane into ascending
-// order.  MISORT_SORT_OEM: Batcher's odd-even merge sort (191 compare-exchanges
-// in the same 15 steps) instead of the bitonic stages (240); the steps after
-// it only need each lane's 32 keys ascending.
-#ifndef MISORT_SORT_OEM
-#define MISORT_SORT_OEM 1
-#endif
+// order: Batcher's odd-even merge sort (191 compare-exchanges in the same 15
+// steps) instead of the bitonic stages (240); the steps after it only need
+// each lane's 32 keys ascending (u32 tile 3.36 -> 3.33 ms at 2^30, u64 -2.4 %,
+// profiles/r05/tile/oem_ab.txt).
 // One step (P, D) of the odd-even merge sort: the pairs (i, i + D) inside
 // one 2P-block, in runs of D starting at D mod P.
 template <typename K, int P, int D>
 __device__ __forceinline__ void oem_step(K (&v)[32]) {
-    if constexpr (sizeof(K) == 8 && MISORT_CX64_ONECMP && MISORT_CX64_BATCH) {
+    if constexpr (sizeof(K) == 8) {
         // u64: the step's compares first, then the selects (as reg_stages_c)
         bool lt[16];
         int q = 0;
@@ -324,7 +317,7 @@ __device__ __forceinline__ void oem_step(K (&v)[32]) {
 }
 template <typename K>
 __device__ __forceinline__ void sort32_regs(K (&v)[32]) {
-    if constexpr (MISORT_SORT_OEM) {
+    {
         oem_step<K, 1, 1>(v);
         oem_step<K, 2, 2>(v);
         oem_step<K, 2, 1>(v);
@@ -340,12 +333,6 @@ __device__ __forceinline__ void sort32_regs(K (&v)[32]) {
         oem_step<K, 16, 4>(v);
         oem_step<K, 16, 2>(v);
         oem_step<K, 16, 1>(v);
-    } else {
-        reg_stages_c<K, 0, 1, true>(v);
-        reg_stages_c<K, 1, 2, true>(v);
-        reg_stages_c<K, 2, 3, true>(v);
-        reg_stages_c<K, 3, 4, true>(v);
-        reg_stages_c<K, 4, 5, true>(v);
     }
 }
 
@@ -375,9 +362,6 @@ __device__ __forceinline__ void phase_c(K* s, int t) {
 // drift apart, overlapping one wave's LDS traffic with another's min/max; a
 // barrier remains around every phase whose window reaches bit 11.
 constexpr int WAVE_BITS = 11;
-#ifndef MISORT_SORT_WAVE_SYNC
-#define MISORT_SORT_WAVE_SYNC 1
-#endif
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
 // Strides HI..STOP (flip first); NEXT_HI: top bit of the phase after the range
@@ -389,7 +373,7 @@ __device__ __forceinline__ void lds_range_w(K* s, int t) {
         constexpr int LOWEST = B > STOP ? B : STOP;
         phase_c<K, B, HI - B, HI - LOWEST + 1, FLIP>(s, t);
         constexpr int NXT = LOWEST - 1 >= STOP ? LOWEST - 1 : NEXT_HI;
-        if constexpr (!MISORT_SORT_WAVE_SYNC || HI >= WAVE_BITS || NXT >= WAVE_BITS || NXT < 0) __syncthreads();
+        if constexpr (HI >= WAVE_BITS || NXT >= WAVE_BITS || NXT < 0) __syncthreads();
         else wave_sync();
         lds_range_w<K, LOWEST - 1, STOP, false, NEXT_HI>(s, t);
     }
@@ -418,20 +402,9 @@ __device__ __forceinline__ void sort_levels_w(K* s, int t) {
 // 5.23 (7), 5.16 (8), 5.21 (9), 5.57 ms (all LDS; profiles/r01/ab/wave_levels.txt).  Default: levels 6..8 in
 // the wave (quad_perm / row_half_mirror only), 9..15 in LDS phases.
 // (Semantics of every cross-lane op: tools/dpp_probe.hip.)
-// Probe-only (tools/build_variant.sh): last level the u32 SORT pass's LDS
-// phases run (15 = the whole tile; smaller values time the tile's lower levels
-// and do not sort).
-#ifndef MISORT_SORT_TOP
-#define MISORT_SORT_TOP 15
-#endif
-// Probe-only (tools/build_variant.sh): last level the u64 SORT tile's LDS phases run.
-#ifndef MISORT_SORT_TOP_U64
-#define MISORT_SORT_TOP_U64 99
-#endif
-// highest level run in the wave (6..11); the levels above go through LDS phases
-#ifndef MISORT_WAVE_LEVELS
-#define MISORT_WAVE_LEVELS 8
-#endif
+// highest level run in the wave (6..11); the levels above go through LDS
+// phases (7 / 9 measured equal or slower, profiles/r03/ab_wl)
+constexpr int WAVE_LEVELS = 8;
 
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
     return max(min(a, b), min(max(a, b), c));  // v_med3_u32
@@ -553,15 +526,14 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
     }
 }
 
-// The SORT tile's top levels as merge levels.  MISORT_SORT_MERGE (u32) /
-// MISORT_SORT_MERGE_U64 = F: levels 1..F-1 run as the bitonic network
+// The SORT tile's top levels as merge levels.  SORT_MERGE_F (u32) /
+// SORT_MERGE_F_U64 = F: levels 1..F-1 run as the bitonic network
 // (registers, DPP, wave-local LDS phases), leaving sorted runs of 2^(F-1) keys
 // (F <= 12: a run lies inside one wave's 2^11 keys); the runs are laid out
 // plainly in LDS with sentinels after each and merged pairwise in levels
 // F..LT by the multi-way pass's in-LDS machinery (lds_merge.h: phased co-rank
 // searches, merge chains), IT outputs per lane -- instead of barrier-separated
-// LDS phases with LT - F + 1 .. LT stages each.  0 = the network for every
-// level.  Measured on one box each (profiles/r04/sortmerge, sortmerge64):
+// LDS phases with LT - F + 1 .. LT stages each.  Measured on one box each (profiles/r04/sortmerge, sortmerge64):
 //   u32 2^14 tile (the default tile from 2^25, see sort_tile_u32): the 2^30
 //   SORT pass 4.31 ms as a network -> 3.61 (F = 12) -> 3.42 (F = 11) ->
 //   3.60 (F = 10); the 2^15 tile with F = 12: 5.80 (one workgroup per CU).
@@ -571,73 +543,44 @@ __device__ __forceinline__ void final_store(const K* s, K* out, int64_t tile, in
 // The merge-level tiles run one tile per workgroup: the merge keeps IT more
 // keys per lane live than the network, and the persistent grid's prefetch
 // measured slower.
-#ifndef MISORT_SORT_MERGE
-#define MISORT_SORT_MERGE 11
-#endif
-#ifndef MISORT_SORT_MERGE_U64
-#define MISORT_SORT_MERGE_U64 10
-#endif
+constexpr int SORT_MERGE_F = 11, SORT_MERGE_F_U64 = 10;
 // The u32 merge-level tile's smallest outputs per lane (even: aligned pair
-// writes; 33 = the odd layout measured first).
-#ifndef MISORT_SORT_IT0
-#define MISORT_SORT_IT0 34
-#endif
-// Probe-only (tools/build_variant.sh): the 2^14 tile stops after the load
-// (1), the register/DPP levels (2) or the LDS levels below the merged ones
-// (3) and stores what it has -- the differences price each phase.
-#ifndef MISORT_SORT_STOP
-#define MISORT_SORT_STOP 0
-#endif
-#ifndef MISORT_SORT_ZW
-#define MISORT_SORT_ZW 1
-#endif
-#ifndef MISORT_SORT_CH_U64
-#define MISORT_SORT_CH_U64 0
-#endif
-#ifndef MISORT_SORT_PT
-#define MISORT_SORT_PT 0
-#endif
-// the merge levels' pair of a lane by its position over the level's constant
-// pair stride (all the tile's runs have one length)
-#ifndef MISORT_SORT_UNIGEO
-#define MISORT_SORT_UNIGEO 1
-#endif
+// writes; 34 = the odd-half layout: IT / 2 = 17 keeps the lanes' chain
+// pointers on distinct banks; 33, the odd layout, measured first,
+// profiles/r04/sorteven).  The merge levels use the multi-way passes' zero
+// words (lds_merge.h, profiles/r05/zwpt) and the uniform pair geometry: all
+// the tile's runs have one length, so a lane's pair is its position over the
+// level's constant pair stride (u32 tile 3346 -> 3314 us at 2^30; u64 +14 us,
+// kept off; profiles/r05/tile/unigeo_ab.txt).  u64 merges one key per LDS read
+// (two-key chains measured equal, profiles/r05/mergek/u64_chain_ab.txt).
+constexpr int SORT_IT0 = 34;
 template <typename KEY, int LT, int F>
 struct SortMergeShape {
     static_assert(F >= 7 && F <= 12 && F <= LT, "merge levels from runs of 64 .. 2^11 keys");
     static constexpr int NT = 1 << (LT - 5);  // 32 keys per lane
     static constexpr int K = 1 << (LT - F + 1), LKS = LT - F + 1, RUN = 1 << (F - 1);
-    // two-key chains for u32, one key per read for u64 (MISORT_SORT_CH_U64)
-    static constexpr int CH = sizeof(KEY) == 4 ? 1 : MISORT_SORT_CH_U64;
+    // two-key chains for u32, one key per read for u64
+    static constexpr int CH = sizeof(KEY) == 4 ? 1 : 0;
     // outputs per lane: the smallest count from IT0 up (step 2) whose level
     // layouts fit: 2^LT keys + per pair G + QA gap.  u32: even (IT0 = 34),
     // so every level writes aligned pairs; u64: odd (33: lanes' diagonals on
     // distinct banks; a pair of u64 keys is a 16-byte write, no cheaper than two)
-    static constexpr int IT0 = CH == 1 ? (sizeof(KEY) == 4 ? MISORT_SORT_IT0 : 32) : 33;
-    static constexpr int rn(int it) { return CH == 1 ? (it + 1) & ~1 : it; }
-    static constexpr int fit(int it) {
-        return (1 << LT) + (K / 2) * (rn(it) + 1 + it) <= NT * it ? it : fit(it + 2);
-    }
+    static constexpr int IT0 = CH == 1 ? SORT_IT0 : 33;
+    static constexpr int fit(int it) { return (1 << LT) + (K / 2) * (it + 1 + it) <= NT * it ? it : fit(it + 2); }
     static constexpr int IT = fit(IT0);
-    static constexpr int RN = rn(IT);                  // the two-key chain merges an even count
-    static constexpr int G = RN + 1;                   // sentinels after each sequence (a chain reads <= RN past it)
+    static_assert(CH == 0 || IT % 2 == 0, "the two-key chain merges an even count");
+    static constexpr int G = IT + 1;                   // sentinels after each sequence (a chain reads <= IT past it)
     static constexpr int QA = IT;                      // pairs start at lane boundaries
     static constexpr int MAXR = 1 << (LT - 1);         // a last-level pair: two runs of 2^(LT-1)
     static constexpr int GS = G;
     static constexpr int WORDS = NT * IT + G + 8;  // the level layouts (>= K runs of RUN + GS)
     static_assert(K * (RUN + GS) <= WORDS && (1 << LT) + (K / 2) * (G + QA) <= NT * IT, "SORT merge layout");
-    // zero words below the A sequences and the levels' pair table, as in the
-    // multi-way passes (lds_merge.h; MISORT_SORT_ZW, MISORT_SORT_PT): the
-    // table sits past the level layouts, 16-byte aligned
-    static constexpr bool ZW = MISORT_SORT_ZW && CH == 1;
-    static constexpr bool PT = MISORT_SORT_PT && K > 2;
-    // uniform geometry: K runs of RUN keys at a stride of RUN + GS (lds_merge.h
-    // shape_uni); u32 tile 3346 -> 3314 us at 2^30, u64 +14 us (kept off),
-    // profiles/r05/tile/unigeo_ab.txt
-    static constexpr bool UNI = MISORT_SORT_UNIGEO && !PT && sizeof(KEY) == 4;
-    static constexpr int PT_AT = (WORDS + 3) & ~3;
-    static constexpr int PT_WORDS = PT ? (K / 2) * (int)(sizeof(PairRec) / sizeof(KEY)) : 0;
-    static constexpr int ALL_WORDS = PT ? PT_AT + PT_WORDS : WORDS;
+    // zero words below the A sequences (two-key chains) and, u32, the
+    // uniform geometry (K runs of RUN keys at a stride of RUN + GS;
+    // lds_merge.h shape_uni)
+    static constexpr bool ZW = CH == 1;
+    static constexpr bool UNI = sizeof(KEY) == 4;
+    static constexpr int ALL_WORDS = WORDS;
 };
 
 // Levels F..LT of a tile whose runs of 2^(F-1) keys are sorted in the padded
@@ -670,12 +613,10 @@ __device__ __forceinline__ void tile_merge_top(KEY* s, int t) {
         st[q] = q * (MS::RUN + MS::GS);
         ln[q] = MS::RUN;
     }
-    PairRec* pt = MS::PT ? reinterpret_cast<PairRec*>(s + MS::PT_AT) : nullptr;
-    lds_merge_prologue<KEY, MS>(s, st, ln, pt, t);
+    lds_merge_prologue<KEY, MS>(s, st, t);
     lds_barrier();
-    KEY r[MS::RN];
-    int ex = 0;
-    lds_merge_levels<KEY, MS, 0>(s, st, ln, r, ex, t, MS::WORDS - 1, pt);
+    KEY r[MS::IT];
+    lds_merge_levels<KEY, MS, 0>(s, st, ln, r, t, MS::WORDS - 1);
     if (t * MS::IT < (1 << LT)) {
         if constexpr (MS::CH == 1 && MS::IT % 2 == 0) {
 #pragma unroll
@@ -722,17 +663,17 @@ __device__ __forceinline__ void final_store_plain(const K* s, K* out, int64_t ti
 // tile's loads in flight; otherwise one tile per workgroup.
 // The first level the u64 SORT tile merges in LDS (0: the whole tile is the
 // network): one condition for the kernel and its launcher, so a probe build
-// with a lower MISORT_SORT_TOP_U64 keeps the persistent grid of the network tile.
+// keeps the persistent grid of the network tile.
 template <typename K, int LT>
 constexpr int sort_tile_mf() {
-    return sizeof(K) == 8 && MISORT_SORT_MERGE_U64 > 0 && MISORT_SORT_TOP_U64 >= LT ? MISORT_SORT_MERGE_U64 : 0;
+    return sizeof(K) == 8 && SORT_MERGE_F_U64 <= LT ? SORT_MERGE_F_U64 : 0;
 }
 
 template <typename K, int LT, bool ORD, bool PERSIST>
 __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU)) void k_sort_tile(
     const K* in, K* out, int64_t n, int64_t ntiles, void* fence, int flk) {
     typedef TileGeo<K, LT> G;
-    // MISORT_SORT_MERGE_U64 = F: levels F..LT as in-LDS merge levels
+    // SORT_MERGE_F_U64 = F: levels F..LT as in-LDS merge levels
     constexpr int MF = sort_tile_mf<K, LT>();
     typedef SortMergeShape<K, LT, MF ? MF : 12> MS;
     // MERGE: 2 keys below the tile (a co-rank probe may read index -1; 16-byte alignment)
@@ -775,14 +716,13 @@ __global__ __launch_bounds__((TileGeo<K, LT>::NT), (TileGeo<K, LT>::WAVES_PER_EU
 #pragma unroll
             for (int c = 0; c < 32; ++c) s[a0 + c] = v[c];
         }
-        if constexpr (MISORT_SORT_WAVE_SYNC) wave_sync();  // level 6 stays inside the wave
-        else __syncthreads();
+        wave_sync();  // level 6 stays inside the wave
         if constexpr (MF > 0) {
             sort_levels_w<K, 6, MF - 1>(s, t);
             tile_merge_top<K, LT, MF>(s, t);
             final_store_plain<K, LT>(s, out, tile, n, full, t, fence, flk);
         } else {
-            sort_levels_w<K, 6, (sizeof(K) == 8 && MISORT_SORT_TOP_U64 < LT ? MISORT_SORT_TOP_U64 : LT)>(s, t);
+            sort_levels_w<K, 6, LT>(s, t);
             final_store<K, LT>(s, out, tile, n, full, t, fence, flk);
         }
         __syncthreads();
@@ -815,7 +755,7 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
     typedef TileGeo<K, LT> G;
     static int64_t cap = 0;  // resident workgroups
     const int64_t ntiles = (n + G::T - 1) >> LT;
-    // the merge-level tile runs one tile per workgroup (see MISORT_SORT_MERGE)
+    // the merge-level tile runs one tile per workgroup (see SORT_MERGE_F)
     const bool persist = sort_tile_mf<K, LT>() == 0 && plan_knobs().persist_sort((int)sizeof(K));
     if (persist && cap == 0) {
         int per_cu = 0, cus = 0, dev = 0;
@@ -837,7 +777,7 @@ void launch_sort_tile(const K* in, K* out, int64_t n, hipStream_t s, void* fence
 
 // ------------------------------------------------ u32 SORT pass kernel
 //
-// The u32 SORT tile (in-wave levels 1..MISORT_WAVE_LEVELS, LDS phases above),
+// The u32 SORT tile (in-wave levels 1..WAVE_LEVELS, LDS phases above),
 // with the full/partial tile split made at compile time: the persistent grid
 // walks only full tiles, and a one-workgroup launch sorts the partial last
 // tile.  With bounds-checked load/store paths inside the persistent loop the
@@ -869,10 +809,10 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
     typedef uint32_t K;
     typedef TileGeo<K, LT> G;
     static_assert(LT == 14 || LT == 15, "u32 SORT tiles");
-    constexpr int WL = MISORT_WAVE_LEVELS;
+    constexpr int WL = WAVE_LEVELS;
     static_assert(G::LOADS == 8 && (G::NT == 1024 || G::NT == 512) && WL >= 5 && WL <= 10, "u32 SORT tile shape");
-    constexpr int MF = MISORT_SORT_MERGE;  // first merged level (0: none)
-    constexpr bool MERGE = MF > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
+    constexpr int MF = SORT_MERGE_F;  // first merged level
+    constexpr bool MERGE = LT == SORT_LT_MERGE;
     typedef SortMergeShape<K, LT, MERGE ? MF : 12> MS;
     // MERGE: 4 words below the tile (a co-rank probe may read index -1)
     __shared__ __attribute__((aligned(16))) K sbuf[(MERGE ? (MS::ALL_WORDS > lds_words(G::T) ? MS::ALL_WORDS
@@ -898,8 +838,7 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
         }
         if constexpr (MERGE) lds_barrier();  // no wait for the previous tile's stores
         else __syncthreads();
-        constexpr int STOP = MERGE ? MISORT_SORT_STOP : 0;
-        if constexpr (STOP == 0 || STOP >= 2) {
+        {
             uint32_t x[32];
 #pragma unroll
             for (int c = 0; c < 32; ++c) x[c] = s[a0 + c];
@@ -909,7 +848,7 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
             // next phase (level WL+1 <= 11) stays inside the wave
 #pragma unroll
             for (int c = 0; c < 32; ++c) s[a0 + c] = x[c];
-            if constexpr (WL + 1 <= WAVE_BITS && MISORT_SORT_WAVE_SYNC) wave_sync();
+            if constexpr (WL + 1 <= WAVE_BITS) wave_sync();
             else __syncthreads();
         }
         // the next tile's loads fly during the LDS phases (issued here, not
@@ -918,15 +857,11 @@ __global__ __launch_bounds__(1 << (LT - 5), LT == 14 ? 4 : 1) void k_sort_u32(
         const int64_t nxt = tile + gridDim.x;
         if (PERSIST && nxt < ntiles) sort_fetch<LT, FULL>(pre, in, nxt, n, t);
         if constexpr (MERGE) {
-            if constexpr (STOP == 0 || STOP >= 3) sort_levels_w<K, WL + 1, (MERGE ? MF : 12) - 1>(s, t);
-            if constexpr (STOP == 0) {
-                tile_merge_top<K, LT, (MERGE ? MF : 12)>(s, t);
-            } else {
-                __syncthreads();
-            }
+            sort_levels_w<K, WL + 1, MF - 1>(s, t);
+            tile_merge_top<K, LT, MF>(s, t);
             final_store_plain<K, LT>(s, out, tile, n, FULL, t, fence, flk);
         } else {
-            sort_levels_w<K, WL + 1, (MISORT_SORT_TOP < LT ? MISORT_SORT_TOP : LT)>(s, t);
+            sort_levels_w<K, WL + 1, LT>(s, t);
             final_store<K, LT>(s, out, tile, n, FULL, t, fence, flk);
         }
         if constexpr (!PERSIST) break;
@@ -942,8 +877,8 @@ template <int LT>
 void launch_sort_u32(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s, uint64_t* fence = nullptr,
                      int flk = 0, hipEvent_t ea = nullptr, hipEvent_t eb = nullptr) {
     constexpr int NT = TileGeo<uint32_t, LT>::NT;
-    // the merge-level tile runs one workgroup per tile (see MISORT_SORT_MERGE)
-    constexpr bool MERGE = MISORT_SORT_MERGE > 0 && LT == SORT_LT_MERGE && MISORT_SORT_TOP >= LT;
+    // the merge-level tile runs one workgroup per tile (see SORT_MERGE_F)
+    constexpr bool MERGE = LT == SORT_LT_MERGE;
     static int64_t cap = 0;
     const int64_t nfull = n >> LT;
     // (on the persistent grid with the next tile's loads in flight it spills

@@ -162,13 +162,11 @@ __global__ __launch_bounds__(SCN) void k_scan_chunks(uint32_t* __restrict__ csum
 // BPW consecutive blocks per workgroup, all their key loads issued before the
 // first block is packed: a block alone is a short chain of dependent steps
 // (loads, LDS, pack, stores), so one per workgroup left the pass latency-bound
-// at eight blocks in flight per CU (MISORT_CODEC_BPW; 1 = one block).
+// at eight blocks in flight per CU (CODEC_BPW; 1 = one block).
 // Measured (profiles/r05/codec/ab.txt, k = 2^26 u32): encode 0.156 -> 0.141 ms,
 // decode 0.122 -> 0.106 ms with 4; 8 was slower; u64 keys keep one block (the
 // pack equal, the decode's 33 KB of staged payload per workgroup 1.5x slower).
-#ifndef MISORT_CODEC_BPW
-#define MISORT_CODEC_BPW 4
-#endif
+constexpr int CODEC_BPW = 4;
 template <typename K, int BPW>
 __global__ __launch_bounds__(CT) void k_codec_pack(const K* __restrict__ kbase, const int64_t* __restrict__ run,
                                                    const uint32_t* __restrict__ off, const uint32_t* __restrict__ coff,
@@ -356,7 +354,7 @@ hipError_t codec_encode_dev(const K* base, const int64_t* run, int64_t n_max, ui
     k_codec_width<K><<<(unsigned)nb, CT, 0, s>>>(base, run, words, wid);
     k_scan_words<<<(unsigned)nc, SCN, 0, s>>>(words, nb, off, csum);
     k_scan_chunks<<<1, SCN, 0, s>>>(csum, nc, run, (int)(sizeof(K) / 4), sizes);
-    constexpr int BPW = sizeof(K) == 4 ? MISORT_CODEC_BPW : 1;  // u64: equal (pack) / slower (unpack)
+    constexpr int BPW = sizeof(K) == 4 ? CODEC_BPW : 1;  // u64: equal (pack) / slower (unpack)
     k_codec_pack<K, BPW><<<(unsigned)((nb + BPW - 1) / BPW), CT, 0, s>>>(base, run, off, csum, wid, out);
     return hipGetLastError();
 }
@@ -374,7 +372,7 @@ hipError_t codec_encode(const K* keys, int64_t n, uint32_t* out, void* scratch, 
 template <typename K>
 hipError_t codec_decode(const uint32_t* in, int64_t n, K* keys, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    constexpr int BPW = sizeof(K) == 4 ? MISORT_CODEC_BPW : 1;  // u64: 33 KB of payload LDS per workgroup
+    constexpr int BPW = sizeof(K) == 4 ? CODEC_BPW : 1;  // u64: 33 KB of payload LDS per workgroup
     k_codec_unpack<K, BPW><<<(unsigned)((codec_blocks(n) + BPW - 1) / BPW), CT, 0, s>>>(in, n, keys);
     return hipGetLastError();
 }

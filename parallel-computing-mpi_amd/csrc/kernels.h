@@ -11,15 +11,10 @@ namespace misort {
 
 // IEEE double bits <-> order-preserving u64 (negative: all bits flipped; else
 // the sign bit set), so every kernel compares unsigned integers.
-#ifndef MISORT_ORD_NOP
-#define MISORT_ORD_NOP 0  // probe builds only: no mapping (wrong for negative doubles)
-#endif
 __device__ __forceinline__ uint64_t ord_of_f64(uint64_t b) {
-    if (MISORT_ORD_NOP) return b;
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 __device__ __forceinline__ uint64_t f64_of_ord(uint64_t o) {
-    if (MISORT_ORD_NOP) return o;
     return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
 }
 
@@ -157,13 +152,10 @@ hipError_t merge_levelk(const uint64_t* src, uint64_t* dst, int64_t n, int lw, i
                         bool gather, int lk_next, LaunchHook* hook = nullptr, bool ord_out = false);
 int64_t mergek_chunks(int64_t n, int lw, int lk, int key_bytes);
 // Fence stride of the multi-way passes (log2 keys).
-#ifndef MISORT_MK_FG_LOG2
-#define MISORT_MK_FG_LOG2 7
-#endif
-constexpr int MERGEK_FENCE_LOG2 = MISORT_MK_FG_LOG2;
+constexpr int MERGEK_FENCE_LOG2 = 7;  // runsk_fg6.hip: 6 (fence stride 256 measured equal to 128, profiles/r02)
 // log2 keys of the u32 SORT tiles (bitonic.h).  15: 1024 lanes, one
 // workgroup per CU, all 15 levels as the bitonic network.  14: 512 lanes, two
-// workgroups per CU, levels 11..14 as in-LDS merge levels (MISORT_SORT_MERGE).
+// workgroups per CU, levels 11..14 as in-LDS merge levels (SORT_MERGE_F).
 // The plan picks per size (sort_tile_u32); u32 multi-way passes take runs of
 // 2^14 and up.
 constexpr int SORT_LT_U32 = 15, SORT_LT_MERGE = 14;

@@ -46,26 +46,18 @@ __device__ __forceinline__ KEY lds_ld(uint32_t a) {
 // phase, sum to >= hi - lo + PH.  Probe addresses stay inside [A0 - 1, A0 + LA)
 // and [B0, B0 + LB].
 //
-// Phase (MISORT_MK_PHASE): lane l of each 32-lane LDS group starts its search
-// at lo - (l % 32) (positions <= lo count as true: the answer is >= lo).  With
-// a common start, lanes whose bases differ at a coarse step differ by a
-// multiple of 2 * step, so their A probes land in ONE bank (step >= 16): the
-// searches were k_mergek's largest LDS cost (SQ probe modes,
-// profiles/r04/sq_attr: 5 conflict cycles per probe instruction, more wave
-// cycles than the merge chains).  The phases put those probes on distinct
-// banks, and the B probes at (IT + 1) * l on distinct banks too.  Measured
-// on one box (profiles/r04/phase): u32 k_mergek 2524 -> 2435 us per 2^30
-// pass, 571 -> 545 at 2^28 (SQ: 3.1 -> 1.6 conflict cycles per search probe);
-// u64 (two-bank keys, 4 waves per SIMD) 2667 -> 2739 us, so u64 keeps a
-// common start.
-#ifndef MISORT_MK_PHASE
-#define MISORT_MK_PHASE 1
-#endif
-// 2: clamped probes, one compare per step (co_rank); 1: the range checks as
-// exec-mask branches (round 3)
-#ifndef MISORT_MK_COR
-#define MISORT_MK_COR 2
-#endif
+// Phase: lane l of each 32-lane LDS group starts its search at lo - (l %
+// 32) (positions <= lo count as true: the answer is >= lo).  With a common
+// start, lanes whose bases differ at a coarse step differ by a multiple of 2 *
+// step, so their A probes land in ONE bank (step >= 16): the searches were
+// k_mergek's largest LDS cost (SQ probe modes, profiles/r04/sq_attr: 5
+// conflict cycles per probe instruction).  The phases put those probes on
+// distinct banks, and the B probes at (IT + 1) * l on distinct banks too:
+// u32 k_mergek 2524 -> 2435 us per 2^30 pass (profiles/r04/phase); u64
+// (two-bank keys, 4 waves per SIMD) measured 2667 -> 2739 us, so u64 keeps a
+// common start.  Every probe is clamped into [lo, hi] and both loads are
+// unconditional, one compare per step, no exec-mask branches (2274 -> 2144 us,
+// profiles/r04/cor2).
 // ZW (zero word): the word before every A sequence holds 0, a key <= every
 // key (and B[LB] is a sentinel), so the probe at lo holds through the data:
 // no i == lo test.  The probes then run on byte addresses of A (j = &A[i-1]; B's
@@ -76,7 +68,7 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     // first co-rank step: the largest power of two <= MAXR + PH (MAXR: a
     // compile-time bound on hi - lo, the steps must be powers of two for the
     // lifting search); steps above maxr + PH (uniform) are skipped
-    constexpr int PH = MISORT_MK_PHASE && sizeof(KEY) == 4 ? 31 : 0;
+    constexpr int PH = sizeof(KEY) == 4 ? 31 : 0;
     constexpr int CO_STEP0 = 1 << (31 - __builtin_clz((unsigned)(MAXR + PH)));
     static_assert(MAXR + PH <= 2 * CO_STEP0 - 1, "co-rank steps cover the range");
     const int lo = d - LB > 0 ? d - LB : 0;
@@ -84,7 +76,7 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
     const KEY* a = s + A0 - 1;
     const KEY* b = s + B0 + d;
     int base = lo - (PH ? (int)(__lane_id() & 31) : 0);
-    if constexpr (ZW && MISORT_MK_COR == 2) {
+    if constexpr (ZW) {
         constexpr int W = (int)sizeof(KEY), WL = W == 4 ? 2 : 3;
         const int ab = (int)lds_addr<KEY>(a);
         const int C = ab + (int)lds_addr<KEY>(b);  // b[-i] at C - &a[i]
@@ -101,40 +93,22 @@ __device__ __forceinline__ int co_rank(const KEY* s, int A0, int LA, int B0, int
         }
         base = (jb - ab) >> WL;
         return base > lo ? base : lo;
-    }
-    if constexpr (MISORT_MK_COR == 2) {
-        // every probe clamped into [lo, hi], both loads unconditional: a
-        // probe at hi that holds makes hi the answer (later probes repeat
+    } else {
+        // a probe at hi that holds makes hi the answer (later probes repeat
         // it); a step that ends below lo tests lo, which holds by definition
         // (the answer is >= lo) and moves base up to lo, within the steps
-        // left.  No exec-mask branches; with a common start (PH = 0) no step
-        // ends below lo.
+        // left; with a common start (PH = 0) no step ends below lo
 #pragma unroll
         for (int step = CO_STEP0; step >= 1; step >>= 1) {
             if (step > maxr + PH) continue;  // uniform
             const int t = base + step;
-            int i;  // clamp(t, lo, hi) (the compiler emits min + cmp + cndmask)
+            int i;  // clamp(t, lo, hi)
             asm("v_med3_i32 %0, %1, %2, %3" : "=v"(i) : "v"(t), "v"(lo), "v"(hi));
             const bool ok = (PH != 0 && i == lo) | (a[i] <= b[-i]);
             base = ok ? i : base;
         }
         return base > lo ? base : lo;
     }
-#pragma unroll
-    for (int step = CO_STEP0; step >= 1; step >>= 1) {
-        if (step > maxr + PH) continue;  // uniform
-        const int i = base + step;
-        if constexpr (PH) {
-            const int ic = i < lo ? lo : (i < hi ? i : hi);  // v_med3_i32
-            const bool ok = i <= lo || (i <= hi && a[ic] <= b[-ic]);
-            base = ok ? i : base;
-        } else {
-            const int ic = i < hi ? i : hi;
-            const bool ok = i <= hi && a[ic] <= b[-ic];
-            base = ok ? i : base;
-        }
-    }
-    return base;
 }
 
 // IT consecutive outputs from diagonal d of merge(s[A0, A0+LA), s[B0, B0+LB)),
@@ -176,21 +150,15 @@ __device__ __forceinline__ void merge_chain(const KEY* s, int A0, int LA, int B0
     }
 }
 
-// Two consecutive keys at LDS byte address a.  MISORT_MK_CHAIN 2: one
-// ds_read_b64 (u32) / ds_read_b128 (u64) at the key's own alignment -- the
-// type claims the vector's alignment so the compiler selects the single wide
-// read, which the unaligned LDS mode of the HSA queues serves; 1: the
-// compiler's choice for a key-aligned pair (ds_read2_b32 / ds_read2_b64, two
-// LDS accesses).
-template <typename KEY, bool WIDE>
+// Two consecutive keys at LDS byte address a (key-aligned: ds_read2_b32 /
+// ds_read2_b64).  One wide read at the pair's alignment measured far slower
+// (unaligned: 4.3 ms per 2^30 pass; the aligned-pair chain with its early-key
+// handling: 2.26 -> 2.56 ms; profiles/r04/ab_chain, r05/zwpt).
+template <typename KEY>
 __device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
-    if constexpr (WIDE) {
-        return *(const __attribute__((address_space(3))) kvec2<KEY>*)(uintptr_t)a;
-    } else {
-        typedef KEY v2 __attribute__((ext_vector_type(2), aligned(sizeof(KEY))));
-        const v2 v = *(const __attribute__((address_space(3))) v2*)(uintptr_t)a;
-        return kvec2<KEY>{v.x, v.y};
-    }
+    typedef KEY v2 __attribute__((ext_vector_type(2), aligned(sizeof(KEY))));
+    const v2 v = *(const __attribute__((address_space(3))) v2*)(uintptr_t)a;
+    return kvec2<KEY>{v.x, v.y};
 }
 
 // The four keys of two ascending pairs (v0 <= v1, n0 <= n1) in order:
@@ -229,7 +197,7 @@ __device__ __forceinline__ kvec2<KEY> lds_ld2(uint32_t a) {
 // outputs (u32) -- the one-key chain spends six VALU and an LDS read per
 // output.  A side gives at most IT keys, so the G >= IT sentinels after each
 // sequence cover every read.
-template <typename KEY, int IT, bool WIDE, int MAXR, bool ZW = false>
+template <typename KEY, int IT, int MAXR, bool ZW = false>
 __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
                                                 KEY (&r)[IT]) {
     static_assert(IT % 2 == 0, "two outputs per step");
@@ -238,7 +206,7 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     const int ia = co_rank<KEY, MAXR, ZW>(s, A0, LA, B0, LB, dc, maxr);
     constexpr uint32_t B2 = 2 * sizeof(KEY);
     const uint32_t pa = lds_addr<KEY>(s + A0 + ia), pb = lds_addr<KEY>(s + B0 + dc - ia);
-    const kvec2<KEY> a = lds_ld2<KEY, WIDE>(pa), b = lds_ld2<KEY, WIDE>(pb);
+    const kvec2<KEY> a = lds_ld2<KEY>(pa), b = lds_ld2<KEY>(pb);
     // S: the side whose last read key is the smaller (ties: either)
     const bool as = a.y <= b.y;
     uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
@@ -246,7 +214,7 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
     merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
 #pragma unroll
     for (int k = 1; k < IT / 2; ++k) {
-        const kvec2<KEY> n = lds_ld2<KEY, WIDE>(ps);
+        const kvec2<KEY> n = lds_ld2<KEY>(ps);
         ps += B2;
         const bool sw = n.y > v1;
         merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
@@ -254,50 +222,11 @@ __device__ __forceinline__ void merge_chain_blk(const KEY* s, int A0, int LA, in
         pl = sw ? ps : pl;
         ps = t;
     }
-}
-
-// merge_chain_blk with ALIGNED two-key reads (chain 3: one ds_read_b64 for u32,
-// ds_read_b128 for u64, at the pair's own alignment -- the unaligned forms
-// measured 2.2x slower).  Every sequence starts at an even LDS slot, and the
-// lane starts each side at the aligned pair holding its first key: when that
-// key is the pair's second, the pair's first key is an earlier output -- <=
-// every key this lane outputs (A[ia-1] <= B[ib] by the co-rank, B[ib-1] <
-// A[ia] by its maximality) -- so it leaves the merge first.  The lane merges
-// RN >= IT + 2 keys (even); its outputs are r[ex, ex + IT), ex = the early
-// keys (0..2).  A side gives at most RN keys from its pair, so G >= RN
-// sentinels.  IT may be odd (the lanes' diagonals then fall on distinct banks).
-template <typename KEY, int IT, int RN, int MAXR>
-__device__ __forceinline__ int merge_chain_al(const KEY* s, int A0, int LA, int B0, int LB, int d, int maxr,
-                                              KEY (&r)[RN]) {
-    static_assert(RN % 2 == 0 && RN >= IT + 2, "two outputs per step, two early keys");
-    const int tot = LA + LB;
-    const int dc = d < tot ? d : tot;
-    const int ia = co_rank<KEY, MAXR>(s, A0, LA, B0, LB, dc, maxr);
-    const int ib = dc - ia;
-    constexpr uint32_t B2 = 2 * sizeof(KEY);
-    const uint32_t pa = lds_addr<KEY>(s + A0 + (ia & ~1)), pb = lds_addr<KEY>(s + B0 + (ib & ~1));
-    const kvec2<KEY> a = lds_ld2<KEY, true>(pa), b = lds_ld2<KEY, true>(pb);
-    const bool as = a.y <= b.y;
-    uint32_t ps = (as ? pa : pb) + B2, pl = (as ? pb : pa) + B2;
-    KEY v0, v1;
-    merge4(a.x, a.y, b.x, b.y, r[0], r[1], v0, v1);
-#pragma unroll
-    for (int k = 1; k < RN / 2; ++k) {
-        const kvec2<KEY> n = lds_ld2<KEY, true>(ps);
-        ps += B2;
-        const bool sw = n.y > v1;
-        merge4(v0, v1, n.x, n.y, r[2 * k], r[2 * k + 1], v0, v1);
-        const uint32_t t = sw ? pl : ps;
-        pl = sw ? ps : pl;
-        ps = t;
-    }
-    return (ia & 1) + (ib & 1);
 }
 
 // Shape traits the level loop reads with defaults: ZW (a zero word before
-// every A sequence, co_rank without its i == lo test; requires a chain other
-// than 3 and G > the keys a chain reads past a sequence), PT (the level's pair
-// geometry from a table in LDS instead of per-pair selects).
+// every A sequence, co_rank without its i == lo test; G > the keys a chain
+// reads past a sequence).
 template <typename S, typename = void>
 struct shape_zw {
     static constexpr bool v = false;
@@ -305,14 +234,6 @@ struct shape_zw {
 template <typename S>
 struct shape_zw<S, decltype((void)S::ZW)> {
     static constexpr bool v = S::ZW;
-};
-template <typename S, typename = void>
-struct shape_pt {
-    static constexpr bool v = false;
-};
-template <typename S>
-struct shape_pt<S, decltype((void)S::PT)> {
-    static constexpr bool v = S::PT;
 };
 // UNI (the SORT tile's merge levels): all K sequences are S::RUN keys long and
 // sequence q starts at q * (S::RUN + S::GS), so every level's pairs sit at a
@@ -337,12 +258,6 @@ constexpr int uni_stride(int lv) {  // the stride of level lv's outputs (lv >= 1
 template <typename S>
 constexpr int uni_in_stride(int lv) { return lv == 1 ? S::RUN + S::GS : uni_stride<S>(lv - 1); }
 
-// Pair p of a level as the lanes read it from the pair table: A and B
-// (start, length), the output start and length; 8 ints per pair.
-struct PairRec {
-    int A0, LA, B0, LB, Q, LP, pad0, pad1;
-};
-
 // The pair geometry of a level of P pairs over sequences of lengths ln[]:
 // pair p's output starts at qp[p] (a multiple of QA past the previous pair's G
 // sentinels) and holds lp[p] keys; maxr bounds its co-rank range (uniform).
@@ -362,35 +277,14 @@ __device__ __forceinline__ void level_geometry(const int* ln, int P, int (&qp)[S
     }
 }
 
-// The pair table of a level of P pairs whose sequences are st[], ln[]: one
-// lane writes it (uniform values, three 8-byte writes per pair).
-template <typename S>
-__device__ __forceinline__ void write_pair_table(PairRec* pt, const int* st, const int* ln, int P, int tid) {
-    int qp[S::K / 2], lp[S::K / 2], maxr;
-    level_geometry<S>(ln, P, qp, lp, maxr);
-    if (tid == 0) {
-#pragma unroll
-        for (int p = 0; p < S::K / 2; ++p) {
-            if (p >= P) break;
-            int2* e = reinterpret_cast<int2*>(pt + p);
-            e[0] = int2{st[2 * p], ln[2 * p]};
-            e[1] = int2{st[2 * p + 1], ln[2 * p + 1]};
-            e[2] = int2{qp[p], lp[p]};
-        }
-    }
-}
-
 // Before the first level (the caller's barrier follows): for a ZW shape the
 // zero word below the first sequence (those between sequences are the
-// caller's: the last of the G words after each), and the first level's pair
-// table (pt: K / 2 records in LDS, or null).
+// caller's: the last of the G words after each).
 template <typename KEY, typename S>
-__device__ __forceinline__ void lds_merge_prologue(KEY* s, const int (&st)[S::K], const int (&ln)[S::K], PairRec* pt,
-                                                   int tid) {
+__device__ __forceinline__ void lds_merge_prologue(KEY* s, const int (&st)[S::K], int tid) {
     if constexpr (shape_zw<S>::v) {
         if (tid == 0) s[st[0] - 1] = (KEY)0;
     }
-    if constexpr (shape_pt<S>::v && S::K > 2) write_pair_table<S>(pt, st, ln, S::K / 2, tid);
 }
 
 // The in-LDS levels: K sequences at st[q] (length ln[q], each followed by G
@@ -398,26 +292,26 @@ __device__ __forceinline__ void lds_merge_prologue(KEY* s, const int (&st)[S::K]
 // Level lv writes pair p's output at qp[p] (a multiple of QA past the
 // previous pair's sentinels) with G sentinels after it; the last level's
 // outputs stay in registers: lane tid holds outputs [tid * IT, tid * IT + IT)
-// of the merged sequence as r[ex, ex + IT).  S (a shape): K, LKS, NT, IT, G,
-// QA, RN (registers per lane: IT, or more for chains that merge extra keys),
-// CH (chain: 0 one key per read, 1/2 two, 3 aligned pairs), MAXR (bound on a
-// pair's shorter sequence), optionally ZW (shape_zw: G - 1 MAX sentinels and
-// a zero word after each sequence) and PT (shape_pt: the pair table pt).  MODE (probes): 1 = no merging, 2 = first
-// level only, 3 = co-rank searches without chains.  pt (null: per-pair
-// selects, (K/2 - 1) x 6 per lane): the pair table lds_merge_prologue wrote
-// for the first level; each level writes the next one's.  Ends with a barrier
-// after the last level's reads (the caller may then overwrite the LDS).
+// of the merged sequence as r[0, IT).  S (a shape): K, LKS, NT, IT, G, QA,
+// CH (chain: 0 one key per read, 1 two), MAXR (bound on a pair's shorter
+// sequence), optionally ZW (shape_zw: G - 1 MAX sentinels and a zero word
+// after each sequence) and UNI (shape_uni).  MODE (probes,
+// MISORT_MK_PROBE): 1 = no merging, 2 = first level only, 3 = co-rank searches
+// without chains.  The pair of a lane: per-pair selects ((K/2 - 1) x 6 per
+// lane; an LDS pair table measured slower, profiles/r05/zwpt) or, UNI, its
+// position over the level's constant pair stride.  Ends with a barrier after
+// the last level's reads (the caller may then overwrite the LDS).
 template <typename KEY, typename S, int MODE>
-__device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&ln)[S::K], KEY (&r)[S::RN], int& ex,
-                                                 int tid, int LAST, PairRec* pt = nullptr) {
-    constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, RN = S::RN, CH = S::CH;
+__device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&ln)[S::K], KEY (&r)[S::IT], int tid,
+                                                 int LAST) {
+    constexpr int K = S::K, LK = S::LKS, NT = S::NT, IT = S::IT, G = S::G, CH = S::CH;
     constexpr bool ZW = shape_zw<S>::v;
-    // a blk chain reads at most IT keys past a sequence (the one-key chain
+    static_assert(CH == 0 || CH == 1, "one- or two-key chains");
+    // a two-key chain reads at most IT keys past a sequence (the one-key chain
     // IT + 1), so the G-th word after it is free for the next sequence's zero word
-    static_assert(!ZW || ((CH == 1 || CH == 2) && G > IT) || (CH == 0 && G > IT + 1),
+    static_assert(!ZW || (CH == 1 && G > IT) || (CH == 0 && G > IT + 1),
                   "zero words: a sentinel word past the chain's reads");
     constexpr KEY MAXK = KMAX<KEY>;
-    ex = 0;
     const int pos = tid * IT;
     const int wpos = __builtin_amdgcn_readfirstlane(tid & ~63) * IT;  // the wave's first lane
 #pragma unroll
@@ -445,19 +339,6 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                 LB = L0;
                 Q = pi * SL;
                 LP = 2 * L0;
-            } else if constexpr (shape_pt<S>::v) {
-                int pi = 0;
-#pragma unroll
-                for (int p = 1; p < K / 2; ++p)
-                    if (p < P) pi += pos >= qp[p] ? 1 : 0;
-                const int2* e = reinterpret_cast<const int2*>(pt + pi);
-                const int2 x = e[0], y = e[1], z = e[2];
-                A0 = x.x;
-                LA = x.y;
-                B0 = y.x;
-                LB = y.y;
-                Q = z.x;
-                LP = z.y;
             } else {
 #pragma unroll
                 for (int p = 1; p < K / 2; ++p) {
@@ -474,7 +355,6 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
         }
         const int end = qp[P - 1] + lp[P - 1];
         if (MODE == 1 || (MODE == 2 && lv > 1) || MODE == 3) {
-            ex = 0;
 #pragma unroll
             for (int j = 0; j < IT; ++j) r[j] = s[pos + j < LAST ? pos + j : LAST];
             if (MODE == 3 && wpos < end) {  // the search alone, its result kept alive
@@ -483,23 +363,18 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
             }
         } else if (wpos < end) {
             if constexpr (CH == 0)
-                merge_chain<KEY, RN, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
-            else if constexpr (CH == 3)
-                ex = merge_chain_al<KEY, IT, RN, S::MAXR>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+                merge_chain<KEY, IT, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
             else
-                merge_chain_blk<KEY, RN, CH == 2, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
+                merge_chain_blk<KEY, IT, S::MAXR, ZW>(s, A0, LA, B0, LB, pos - Q, maxr, r);
         }
         lds_barrier();
         if (lv < LK) {
             // a lane's outputs past its pair's end are MAX (the chain ran into
             // the sentinels), the value the sentinel stores write there too
             if (pos < Q + LP) {
-                if constexpr (CH == 3 || IT % 2) {
-                    // output j is r[ex + j]: one store per key from base pos - ex
-                    KEY* q = s + pos - ex;
+                if constexpr (IT % 2) {
 #pragma unroll
-                    for (int k = 0; k < RN; ++k)
-                        if (k >= ex && k < ex + IT) q[k] = r[k];
+                    for (int k = 0; k < IT; ++k) s[pos + k] = r[k];
                 } else {
 #pragma unroll
                     for (int j = 0; j < IT; j += 2)
@@ -528,11 +403,6 @@ __device__ __forceinline__ void lds_merge_levels(KEY* s, int (&st)[S::K], int (&
                         if (q < P) e = zl == q ? qp[q] : e;
                     s[e - 1] = (KEY)0;
                 }
-            }
-            // the next level's pair table (its sequences: this level's
-            // outputs); every lane read this level's before the barrier above
-            if constexpr (shape_pt<S>::v) {
-                if ((P >> 1) > 1) write_pair_table<S>(pt, qp, lp, P >> 1, tid);
             }
             lds_barrier();
 #pragma unroll

@@ -23,12 +23,6 @@
 #include <mutex>
 
 // Build-time A/B switches (tools/build_variant.sh): non-temporal tile loads / stores.
-#ifndef MISORT_RUN_NT_LOAD
-#define MISORT_RUN_NT_LOAD 1
-#endif
-#ifndef MISORT_RUN_NT_STORE
-#define MISORT_RUN_NT_STORE 1
-#endif
 
 namespace misort {
 namespace {
@@ -176,11 +170,7 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
         for (int k = 0; k < IT; ++k) {
             const int e = k * NT + tid;
             const K* q = e < la ? A + e : B + (e - la);
-#if MISORT_RUN_NT_LOAD
             x[k] = e < len ? __builtin_nontemporal_load(q) : KT_MAX<K>;
-#else
-            x[k] = e < len ? *q : KT_MAX<K>;
-#endif
         }
 #pragma unroll
         for (int k = 0; k < IT; ++k) s[k * NT + tid] = x[k];
@@ -229,11 +219,7 @@ __global__ __launch_bounds__(NT) void k_runs_merge(const K* __restrict__ src, K*
 #pragma unroll
         for (int k = 0; k < IT / V; ++k) {
             const int e = (k * NT + tid) * V;
-#if MISORT_RUN_NT_STORE
             __builtin_nontemporal_store(*reinterpret_cast<const vec*>(s + e), reinterpret_cast<vec*>(out + e));
-#else
-            *reinterpret_cast<vec*>(out + e) = *reinterpret_cast<const vec*>(s + e);
-#endif
         }
     } else {
         for (int k = tid; k < len; k += NT) out[k] = s[k];
@@ -291,9 +277,6 @@ hipError_t merge_level_it(const K* src, K* dst, int64_t n, int lw, hipStream_t s
 }
 
 // Merge levels over at most RUN_SMALL_N keys use 256-lane tiles when set.
-#ifndef MISORT_RUN_SMALL_TILES
-#define MISORT_RUN_SMALL_TILES 1
-#endif
 constexpr int64_t RUN_SMALL_N = (int64_t)1 << 20;
 
 int env_knob(const char* k) {
@@ -335,7 +318,7 @@ hipError_t merge_level(const K* src, K* dst, int64_t n, int lw, hipStream_t s, i
     // small levels (the fence merges of small sorts: 2^17 u64 fences at 2^24 u32
     // keys are 16 default tiles) take 4x smaller tiles, so more CUs share them
     const bool fuse = run_fuse_knob() == 2 || (run_fuse_knob() == 1 && n <= RUN_SMALL_N);
-    if (MISORT_RUN_SMALL_TILES && n <= RUN_SMALL_N && NT > 256 && ((int64_t)1 << lw) >= 256 * IT)
+    if (n <= RUN_SMALL_N && NT > 256 && ((int64_t)1 << lw) >= 256 * IT)
         return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);
     if (((int64_t)1 << lw) >= NT * IT) return merge_level_it<K, NT, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);
     return merge_level_it<K, 256, IT>(src, dst, n, lw, s, o0, o1, fuse, hook);  // runs shorter than the default tile

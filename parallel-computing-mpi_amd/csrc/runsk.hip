@@ -57,10 +57,27 @@ namespace {
 #endif
 constexpr int FG_LOG2 = MISORT_RUNSK_FGL;
 constexpr int64_t FG = (int64_t)1 << FG_LOG2;  // fence stride (keys)
-#ifndef MISORT_MK_NT
-#define MISORT_MK_NT 512
-#endif
 typedef unsigned __int128 u128;
+
+// The first fence merge levels of a pass as LDS merge levels (k_fence_merge)
+// when the pass has at least FENCE_MERGE_MIN_BLOCKS sub-groups; else ranks by
+// binary searches (k_fence_lds), which can split a sub-group over several
+// blocks.  Measured (profiles/r03/ab3): 2^30 u32 66.5 -> 67.0 Gkeys/s, 2^26
+// 61.5 -> 62.1; at 2^24 (64 and 16 sub-groups) the merge was slower.
+constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
+// bytes of the aligned window k_bounds reads around its interpolated guess
+// (64: u32 passes -1..-10 us, u64 +2 us, profiles/r05/plan/bl64_ab.txt)
+constexpr int BOUNDS_LINE = 128;
+// k_bounds loads the scanned fence counts beside the chunk-start fence (one
+// dependent round less) and divides chunk indices in 32 bits: 2^30 pass -2 to
+// -8 us, 2^28 and u64 equal (profiles/r05/plan/bearly_ab.txt).
+// u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
+// VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
+// (profiles/r03/ab1).  The in-LDS levels read two keys per LDS read for u32
+// (merge_chain_blk; 1999 -> 1969 us, profiles/r04/ab_chain) and one for u64
+// (merge_chain: the two-key chain measured equal in the tile, -6 % in the
+// passes, profiles/r05/mergek/u64_chain_ab.txt); zero words below the A
+// sequences for the two-key chain (profiles/r05/zwpt).
 
 // Per key type: the fence type (key bits above 32 bits of run and position),
 // the chunk workgroup (NT lanes x IT keys: CAP keys a chunk at most), the
@@ -68,143 +85,53 @@ typedef unsigned __int128 u128;
 // merged in LDS (64 KiB).
 template <typename KEY>
 struct KTr;
-// Build-time probes (tools/build_variant.sh): the u32 chunk capacity and the
-// workgroups per CU its LDS tile allows.
-#ifndef MISORT_MK_CAP
-#define MISORT_MK_CAP 0
-#endif
-#ifndef MISORT_MK_WGCU
-#define MISORT_MK_WGCU 0
-#endif
-#ifndef MISORT_MK_IT
-#define MISORT_MK_IT 0  // u32 outputs per lane of a merge level (0: 18 at >= 512 lanes)
-#endif
-// The first fence merge levels of a pass as LDS merge levels (k_fence_merge)
-// when set and the pass has at least FENCE_MERGE_MIN_BLOCKS sub-groups; else
-// ranks by binary searches (k_fence_lds), which can split a sub-group over
-// several blocks.  Measured (profiles/r03/ab3): 2^30 u32 66.5 -> 67.0 Gkeys/s,
-// 2^26 61.5 -> 62.1; at 2^24 (64 and 16 sub-groups) the merge was slower
-// (39.0 -> 38.4).
-#ifndef MISORT_FENCE_MERGE
-#define MISORT_FENCE_MERGE 1
-#endif
-// bytes of the aligned window k_bounds reads around its interpolated guess
-// (64: u32 passes -1..-10 us, u64 +2 us, profiles/r05/plan/bl64_ab.txt -- noise level)
-#ifndef MISORT_BOUNDS_LINE
-#define MISORT_BOUNDS_LINE 128
-#endif
-// k_bounds loads the scanned fence counts beside the chunk-start fence (one
-// dependent round less) and divides chunk indices in 32 bits: 2^30 pass -2 to
-// -8 us, 2^28 and u64 equal (profiles/r05/plan/bearly_ab.txt).
-constexpr int64_t FENCE_MERGE_MIN_BLOCKS = 128;
-// u32 k_mergek loads its rows straight into LDS (global_load_lds_dword: no
-// VGPR staging, no ds_write per key): 2^30 k_mergek 2.034 -> 1.997 ms per pass
-// (profiles/r03/ab1); 0 = loads into registers, then ds_write.
-#ifndef MISORT_MK_ZW
-#define MISORT_MK_ZW 1
-#endif
-// zero words for the one-key chain too (the u64 passes; one more sentinel word)
-#ifndef MISORT_MK_ZW_CH0
-#define MISORT_MK_ZW_CH0 0
-#endif
-
-#ifndef MISORT_MK_PT
-#define MISORT_MK_PT 0
-#endif
-#ifndef MISORT_MK_GLDS
-#define MISORT_MK_GLDS 1
-#endif
-// k_mergek stages a chunk whose output shift is even with pair writes.
-#ifndef MISORT_MK_PAIRSTAGE
-#define MISORT_MK_PAIRSTAGE 1
-#endif
-// The in-LDS merge levels of k_mergek: 0 = one key per LDS read (merge_chain),
-// 1 / 2 = two keys per read (merge_chain_blk; 1: ds_read2_b32 / ds_read2_b64,
-// 2: one unaligned ds_read_b64 / ds_read_b128).  Measured at 2^30 u32
-// (profiles/r04/ab_chain): k_mergek 1999 -> 1969 us with 1; 2 takes 4329 us
-// -- unaligned wide LDS reads are far slower than their bank model (the SQ
-// counts fewer bank-conflict cycles) -- and u64 with 2 16.7 -> 21.3 ms.
-#ifndef MISORT_MK_CHAIN
-#define MISORT_MK_CHAIN 1
-#endif
-#ifndef MISORT_MK_CHAIN_U64
-#define MISORT_MK_CHAIN_U64 0
-#endif
-// 16-way u32 passes: larger chunks.  A chunk holds FM * FG = CAP - K * FG
-// keys on average, so at K = 16 a quarter of an 8192-key chunk's lanes idle.
-// Round 4: 22 outputs per lane (CAP 10752, three workgroups per CU) measured
-// 2^30 68.9 -> 69.8 Gkeys/s; 20 or 24 per lane were slower -- an EVEN half
-// (IT / 2 = 10 or 12) puts the lanes' chain pointers, IT / 2 apart, on a few
-// banks.  Round 6: 26 outputs per lane (IT / 2 = 13, odd) and the LDS sized by
-// the larger of the segments and the level outputs (not their sum): CAP 12864,
+// u32, 2..8-way passes: 512 lanes x 18 outputs, 8960-key chunks (the largest
+// the 18-output level layout fits: CAP + 4 (G + QA) <= 9216; 8192 before: 2^24
+// +1.5 %, 2^28 +0.8 %, profiles/r04/chunk32), four workgroups per CU; 22
+// outputs per lane at three per CU measured slower (profiles/r06/plan/fg6_ab.txt).
+// 16-way passes: larger chunks.  A chunk holds FM * FG = CAP - K * FG keys on
+// average, so at K = 16 a quarter of an 8192-key chunk's lanes idle.  Round
+// 4: 22 outputs per lane (CAP 10752, three workgroups per CU) measured 2^30
+// 68.9 -> 69.8 Gkeys/s; 20 or 24 per lane were slower -- an EVEN half (IT / 2
+// = 10 or 12) puts the lanes' chain pointers, IT / 2 apart, on a few banks.
+// Round 6: 26 outputs per lane (IT / 2 = 13, odd) and the LDS sized by the
+// larger of the segments and the level outputs (not their sum): CAP 12864,
 // the largest the 26-output level layout holds (CAP + 8 (G + QA) <= 512 * 26),
 // still three workgroups per CU (53.4 KB); 2^30 k_mergek 2154 -> 2049 us,
-// 81.6 -> 84.4 Gkeys/s, 2^28 82.2 -> 84.6 (profiles/r06/mergek/it26_ab.txt).
-#ifndef MISORT_MK_IT16
-#define MISORT_MK_IT16 26
-#endif
-#ifndef MISORT_MK_CAP16
-#define MISORT_MK_CAP16 12864
-#endif
-#ifndef MISORT_MK_WGCU16
-#define MISORT_MK_WGCU16 3
-#endif
-// 16-way passes: keys per load row (a row lies in one segment; the chunk
-// descriptor holds 8 bytes per row).  128 instead of 64 halves the
-// descriptors (1664 -> 896 bytes per chunk): 2^30 u32 pass 2569 -> 2547 us,
-// 2^26 -1.8 %, u64 2^29 -9 us per pass, k_mergek itself equal
-// (profiles/r05/plan/rw_ab.txt).
-#ifndef MISORT_MK_RW16
-#define MISORT_MK_RW16 128
-#endif
+// 81.6 -> 84.4 Gkeys/s, 2^28 82.2 -> 84.6 (profiles/r06/mergek/it26_ab.txt);
+// 768 or 640 lanes at two workgroups per CU were slower (nt_ab.txt).  Load rows
+// of 128 keys (the descriptor holds 8 bytes per row; 64 -> 128 halved it:
+// 2^30 pass 2569 -> 2547 us, profiles/r05/plan/rw_ab.txt).
 template <>
 struct KTr<uint32_t> {
     typedef uint64_t F;
-    static constexpr int NT = MISORT_MK_NT;
-    static constexpr int IT = MISORT_MK_IT ? MISORT_MK_IT : NT >= 512 ? 18 : 9216 / NT;  // NT * IT = 9216 slots per 512 lanes' worth
-    // 8960 at 512 lanes: the largest the 18-output level layout fits (CAP + 4 (G + QA) <= 9216; 8192
-    // before: 2^24 +1.5 %, 2^28 +0.8 %, profiles/r04/chunk32)
-    static constexpr int CAP = MISORT_MK_CAP ? MISORT_MK_CAP : NT == 512 ? 8960 : NT > 512 ? 16 * NT : 8192;
-    static constexpr int WG_PER_CU = MISORT_MK_WGCU ? MISORT_MK_WGCU : NT == 1024 ? 2 : 4;  // ~34 KiB tiles; 8 waves per SIMD at NT = 512
+    static constexpr int NT = 512, IT = 18, CAP = 8960, WG_PER_CU = 4;
+    static constexpr int IT16 = 26, CAP16 = 12864, WG16 = 3;
     // the chunk shape of a pass of lk levels
-    static constexpr bool big(int lk) { return lk == 4 && MISORT_MK_IT16 > 0 && NT == 512; }
-    static constexpr int nt(int) { return NT; }
-    static constexpr int it(int lk) { return big(lk) ? MISORT_MK_IT16 : IT; }
+    static constexpr bool big(int lk) { return lk == 4; }
+    static constexpr int it(int lk) { return big(lk) ? IT16 : IT; }
     // (k_fence_counts keeps 8-bit per-chunk counts: at most 255 + K fences of FG
     // keys a chunk, a bound only the 64-key build can reach)
-    static constexpr int cap16() { return MISORT_MK_CAP16 < (255 + 16) * FG ? MISORT_MK_CAP16 : (255 + 16) * (int)FG; }
+    static constexpr int cap16() { return CAP16 < (255 + 16) * FG ? CAP16 : (255 + 16) * (int)FG; }
     static constexpr int cap(int lk) { return big(lk) ? cap16() : CAP; }
-    static constexpr int wg(int lk) { return big(lk) ? MISORT_MK_WGCU16 : WG_PER_CU; }
+    static constexpr int wg(int lk) { return big(lk) ? WG16 : WG_PER_CU; }
     static constexpr int FL_LDS = 13;                       // 8192 fences = 64 KiB
     static constexpr int LW_MIN = SORT_LT_MERGE, LWK_MAX = 30;  // runs >= the smaller SORT tile; 32-bit row offsets
 };
-static_assert(KTr<uint32_t>::NT == 256 || KTr<uint32_t>::NT == 384 || KTr<uint32_t>::NT == 512 ||
-                  KTr<uint32_t>::NT == 1024,
-              "chunk workgroup");
 // The u64 chunk shape: 18 outputs per lane and the largest capacity whose
 // level layout fits 512 x 18 slots (CAP + 8 (G + QA) <= 9216): 8832 keys
 // (69 fences of 128) instead of 8192 measured 2^29 u64 35.4 -> 36.5-36.7
 // Gkeys/s, k_mergek 2.46 -> 2.33 ms per pass, 2^26 +2.2 %; 9216 keys at 20 per
-// lane was slower (profiles/r04/chunk64).  Build-time probes: tools/build_variant.sh.
-#ifndef MISORT_MK_IT64
-#define MISORT_MK_IT64 18
-#endif
-#ifndef MISORT_MK_CAP64
-#define MISORT_MK_CAP64 8832
-#endif
-#ifndef MISORT_MK_WGCU64
-#define MISORT_MK_WGCU64 2
-#endif
+// lane was slower (profiles/r04/chunk64).  The 64-key build (runsk_fg6.hip)
+// takes 8896 (139 fences of 64): k_mergek -5 us per 2^29 pass
+// (profiles/r05/mergek/cap_ab.txt).
 template <>
 struct KTr<uint64_t> {
     typedef u128 F;
-    static constexpr int NT = 512;
-    static constexpr int IT = MISORT_MK_IT64;
-    static constexpr int CAP = MISORT_MK_CAP64;  // 69 KiB of keys: two tiles per CU, 4 waves per SIMD
-    static constexpr int WG_PER_CU = MISORT_MK_WGCU64;
+    static constexpr int NT = 512, IT = 18, WG_PER_CU = 2;
+    static constexpr int CAP = FG_LOG2 == 6 ? 8896 : 8832;  // ~69 KiB of keys: two tiles per CU, 4 waves per SIMD
     static constexpr int FL_LDS = 12;    // 4096 fences = 64 KiB
     static constexpr int LW_MIN = 13, LWK_MAX = 29;  // runs >= the u64 SORT tile; 32-bit row offsets
-    static constexpr int nt(int) { return NT; }
     static constexpr int it(int) { return IT; }
     static constexpr int cap(int) { return CAP; }
     static constexpr int wg(int) { return WG_PER_CU; }
@@ -221,44 +148,32 @@ constexpr int SCAN_NT_MAX = 256;  // chunks per fence-count block (SCAN_NT below
 template <typename KEY, int LK>
 struct Shape {
     typedef KTr<KEY> T;
-    // the merge chain of the in-LDS levels (MISORT_MK_CHAIN*) and the sentinels
-    // after each sequence: G >= the keys a chain may read past its sequence
-    static constexpr int CH = sizeof(KEY) == 4 ? MISORT_MK_CHAIN : MISORT_MK_CHAIN_U64;
-    static constexpr int NT = T::nt(LK), IT = T::it(LK), CAP = T::cap(LK);
+    // the merge chain of the in-LDS levels: two keys per read (u32), one (u64)
+    static constexpr int CH = sizeof(KEY) == 4 ? 1 : 0;
+    static constexpr int NT = T::NT, IT = T::it(LK), CAP = T::cap(LK);
     static constexpr int MAXR = CAP / 2;  // co-rank range bound: min(LA, LB) <= CAP / 2
-    // chain 3 merges RN = IT + 2 keys rounded up to even (the lane's IT outputs
-    // after up to two early keys) and reads up to RN + 2 - 2 keys past a
-    // sequence start; chains 0-2 read up to IT
-    static constexpr int RN = CH == 3 ? (IT + 3) & ~1 : IT;
-    // zero words below the A sequences (co_rank without its i == lo test;
-    // MISORT_MK_ZW): the last of the G words after a sequence holds the next
+    // zero words below the A sequences (co_rank without its i == lo test; the
+    // two-key chain): the last of the G words after a sequence holds the next
     // one's, so G exceeds the keys a chain reads past a sequence (IT for the
-    // two-key chains, IT + 1 for the one-key chain)
-    static constexpr bool ZW = MISORT_MK_ZW && (CH == 1 || CH == 2 || (CH == 0 && MISORT_MK_ZW_CH0));
-    static constexpr int G = CH == 3 ? RN + 1 : IT + 1 + (ZW && CH == 0 ? 1 : 0);
-    // level outputs start at lane boundaries; chain 3 also needs even slots
-    static constexpr int QA = CH == 3 && (IT & 1) ? 2 * IT : IT;
-    static_assert(CH != 3 || QA % 2 == 0, "chain 3: even sequence starts");
-    static_assert(CH == 3 || IT % 2 == 0, "chains 0-2: outputs stored as aligned pairs");
-    // LDS slot of segment q (o = its first chunk position): chain 3 reads
-    // aligned pairs, so every sequence starts at an even slot
-    __device__ __host__ static int seg(int o, int q) { return CH == 3 ? (o + q * (G + 2) + 1) & ~1 : o + q * G; }
+    // two-key chain, IT + 1 for the one-key chain)
+    static constexpr bool ZW = CH == 1;
+    static constexpr int G = IT + 1;
+    static constexpr int QA = IT;  // level outputs start at lane boundaries
+    static_assert(IT % 2 == 0, "outputs stored as aligned pairs");
+    // LDS slot of segment q (o = its first chunk position)
+    __device__ __host__ static int seg(int o, int q) { return o + q * G; }
     static constexpr int K = 1 << LK, LKS = LK;
-    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk (u32 at 512 lanes: 62 / 60 / 56 / 48)
-    static constexpr int RW = LK == 4 ? MISORT_MK_RW16 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
+    static constexpr int FM = CAP / (int)FG - K;   // fences per chunk, worst case (merge_pass cuts at more)
+    static constexpr int RW = LK == 4 ? 128 : (LK == 3 || NT % 256) ? 128 : 256;  // load row: RW keys of one segment
     static constexpr int NR = NT / RW;             // row parts: waves [p*RW/64, (p+1)*RW/64) load part p
-    // load slots per lane: enough rows for CAP keys in K segments (18 at
-    // CAP = 8192, IT = 17 or 18)
+    // load slots per lane: enough rows for CAP keys in K segments
     static constexpr int LS_ROWS = ((CAP + RW - 1) / RW + K + NR - 1) / NR;
     static constexpr int LS = ((IT + 1) & ~1) <= LS_ROWS ? LS_ROWS : ((IT + 1) & ~1);
     static constexpr int NROWS = LS * NR;           // lane slot j of part p holds row j * NR + p
-    static constexpr int PADK = PAD;  // keys below s (a co-rank probe may read index -1)
     // the tile holds the chunk's segments with their sentinels (CAP + K G) and
     // every level's outputs (<= NT IT slots by the level layout, + G sentinels)
     static constexpr int NB_EXT = CAP + K * G > NT * IT + G ? CAP + K * G : NT * IT + G;
-    static constexpr int LDS_KEYS = CH == 3 ? PAD + CAP + K * (G + QA) + 16 : PAD + NB_EXT + 16;
-    // the levels' pair table in LDS (MISORT_MK_PT)
-    static constexpr bool PT = MISORT_MK_PT && K > 2;
+    static constexpr int LDS_KEYS = PAD + NB_EXT + 16;
     static_assert(FM > 0 && FM < 256 && SCAN_NT_MAX * FM < 65536,
                   "fence stride vs chunk (k_fence_counts keeps 8-bit counts and 16-bit block prefixes)");
     static_assert(CAP <= (NROWS - K) * RW, "segment rows: ceil(l_r / RW) summed over K segments");
@@ -401,10 +316,7 @@ __global__ __launch_bounds__(1024) void k_fence_lds(const FT* __restrict__ F, FT
 // end checks.  k_fence_lds ranks every fence by K - 1 binary searches (56
 // dependent LDS reads per fence at K = 8, runs of 256); a merge level costs a
 // lane about 2 log2(S) reads for FIT outputs.
-#ifndef MISORT_FENCE_FIT
-#define MISORT_FENCE_FIT 8
-#endif
-constexpr int FIT = MISORT_FENCE_FIT;  // 16: 2^30 pass +11..23 us (profiles/r05/plan/fit_ab.txt)
+constexpr int FIT = 8;  // 16: 2^30 pass +11..23 us (profiles/r05/plan/fit_ab.txt)
 template <typename FT>
 __global__ __launch_bounds__(1024) void k_fence_merge(const FT* __restrict__ F, FT* __restrict__ M, int64_t nf,
                                                       int wf_log2, int a) {
@@ -496,49 +408,32 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sw) {
 // fences per lane; else (many blocks) the block's SCAN_NT lanes read the fence
 // range coalesced and add each fence to its chunk's counters with an LDS
 // atomic -- 2^30: 41.5 us, the slices' strided loads 107 us.
-// MISORT_FC_U32: one u32 LDS counter per (chunk, run) (the coalesced path's
-// atomics then collide only between lanes of one chunk and run); 0 = the runs'
-// 8-bit fields packed in two u64 words per chunk (a wave's lanes, mostly in one
-// chunk, all add to one word).
-#ifndef MISORT_FC_U32
-#define MISORT_FC_U32 1
-#endif
-// the coalesced form's fences per lane in flight (their loads issued together;
-// 2^30 pass -7 us, u64 2^29 -10 us, profiles/r05/plan/fcb_ab.txt)
-#ifndef MISORT_FC_BATCH
-#define MISORT_FC_BATCH 8
-#endif
-// lanes of the coalesced form's block (it counts with all of them; the scan
-// uses the first SCAN_NT): 512 instead of 256 measured 2^30 pass -6 us, u64
-// 2^29 -5 us, 2^28 equal (profiles/r05/plan/fcnt_ab.txt).  Reading the whole
-// fence window in k_bounds instead of its interpolated line measured slower at
-// every size (2^30 pass +36 us; profiles/r05/plan/win_ab.txt).
-#ifndef MISORT_FC_NT
-#define MISORT_FC_NT 512
-#endif
-constexpr int COUNT_NT = 1024, FC_NT = MISORT_FC_NT;
+// One u32 LDS counter per (chunk, run): the coalesced path's atomics collide
+// only between lanes of one chunk and run (the runs' 8-bit fields packed in two
+// u64 words per chunk made a wave's lanes, mostly in one chunk, all add to
+// one word; profiles/r03/ab_fc).  The coalesced form keeps FC_BATCH fences per
+// lane in flight (their loads issued together; 2^30 pass -7 us, u64 2^29 -10
+// us, profiles/r05/plan/fcb_ab.txt) and counts with FC_NT lanes (it scans with
+// the first SCAN_NT): 512 instead of 256 measured 2^30 pass -6 us, u64 2^29
+// -5 us (profiles/r05/plan/fcnt_ab.txt).  Reading the whole fence window in
+// k_bounds instead of its interpolated line measured slower at every size
+// (2^30 pass +36 us; profiles/r05/plan/win_ab.txt).
+constexpr int FC_BATCH = 8;
+constexpr int COUNT_NT = 1024, FC_NT = 512;
 static_assert(FC_NT >= SCAN_NT && FC_NT <= COUNT_NT && FC_NT % 64 == 0, "fence-count block");
 template <typename FT, bool SLICES>
 __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict__ M, Geo geo, int64_t nchunks,
                                                            int cpb, int* __restrict__ P, int* __restrict__ bsum,
                                                            int* __restrict__ ovf) {
     __shared__ uint64_t sws[COUNT_NT / 64];
-#if MISORT_FC_U32
     __shared__ uint32_t sc[SCAN_NT][16];
-#else
-    __shared__ unsigned long long sc[SCAN_NT][2];
-#endif
     const int tid = threadIdx.x;
     if (ovf && blockIdx.x == 0 && tid == 0) *ovf = 0;  // the capacity split's list, empty (k_chunk_desc fills it)
     const int64_t c0 = (int64_t)blockIdx.x * cpb, c = c0 + tid;  // cpb <= SCAN_NT chunks per block
     const int64_t c1 = c0 + cpb < nchunks ? c0 + cpb : nchunks;
     const int K = geo.K();
     const int gl = geo.lw + geo.lk;
-#if MISORT_FC_U32
     for (int i = tid; i < SCAN_NT * 16; i += (int)blockDim.x) (&sc[0][0])[i] = 0u;  // SCAN_NT or COUNT_NT lanes
-#else
-    if (tid < SCAN_NT) sc[tid][0] = sc[tid][1] = 0ull;
-#endif
     __syncthreads();
     int64_t g, t;
     chunk_place(geo, c0, g, t);
@@ -558,15 +453,10 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
     };
     // a lane's per-run counts of one chunk (8-bit fields of lo8 / hi8) into its LDS counters
     auto flush = [&](int64_t ch, uint64_t lo8, uint64_t hi8) {
-#if MISORT_FC_U32
         for (int r = 0; r < K; ++r) {
             const uint32_t v = (uint32_t)(((r < 8 ? lo8 : hi8) >> (8 * (r & 7))) & 0xFF);
             if (v) atomicAdd(&sc[ch][r], v);
         }
-#else
-        if (lo8) atomicAdd(&sc[ch][0], lo8);
-        if (hi8) atomicAdd(&sc[ch][1], hi8);
-#endif
     };
     if constexpr (SLICES) {
         const int64_t per = (f1 - f0 + COUNT_NT - 1) / COUNT_NT;
@@ -588,7 +478,7 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
         if (cur >= 0) flush(cur, lo8, hi8);
     } else {
         // FCB fences per lane in flight: their loads first, then their counts
-        constexpr int FCB = MISORT_FC_BATCH;
+        constexpr int FCB = FC_BATCH;
         for (int64_t e0 = f0 + tid; e0 < f1; e0 += FCB * FC_NT) {
             uint32_t tg[FCB];
 #pragma unroll
@@ -601,23 +491,14 @@ __global__ __launch_bounds__(COUNT_NT) void k_fence_counts(const FT* __restrict_
                 const int64_t e = e0 + (int64_t)u * FC_NT;
                 if (e >= f1) break;
                 const int r = (int)((tg[u] >> (32 - geo.lk)) & (K - 1));
-#if MISORT_FC_U32
                 atomicAdd(&sc[chunk_of(e)][r], 1u);
-#else
-                atomicAdd(&sc[chunk_of(e)][r >> 3], 1ull << (8 * (r & 7)));
-#endif
             }
         }
     }
     __syncthreads();
     // scan 4 runs at a time as 16-bit fields of one u64 (block prefixes <=
     // SCAN_NT * FM < 2^16): K/4 block scans instead of K
-#if MISORT_FC_U32
     auto count_of = [&](int q) { return tid < cpb ? (uint64_t)sc[tid][q] : 0ull; };
-#else
-    const uint64_t w8[2] = {tid < cpb ? sc[tid][0] : 0ull, tid < cpb ? sc[tid][1] : 0ull};
-    auto count_of = [&](int q) { return (w8[q >> 3] >> (8 * (q & 7))) & 0xFFull; };
-#endif
     for (int q0 = 0; q0 < K; q0 += 4) {
         uint64_t v = 0;
 #pragma unroll
@@ -734,7 +615,7 @@ __device__ int64_t window_bound(const KEY* __restrict__ src, const typename KTr<
     // before it); otherwise it narrows the range to one side.  It cuts the
     // dependent probe rounds, which pays when many searches share the memory
     // system; a few thousand latency-bound ones run faster without it.
-    constexpr int BW = MISORT_BOUNDS_LINE / (int)sizeof(KEY);
+    constexpr int BW = BOUNDS_LINE / (int)sizeof(KEY);
     const int64_t blk = (p < b ? p : b - 1) & ~(int64_t)(BW - 1);
     bool fwd;
     if (line && a < b && blk + BW <= len && ((uintptr_t)kr & 15) == 0) {
@@ -1152,16 +1033,13 @@ __device__ __forceinline__ V out_vec(V v) {
 
 template <typename KEY, int LK, bool FENCES, int MODE, bool ORD = false>
 __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY* __restrict__ dst,
-                                             typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid,
-                                             PairRec* pt) {
+                                             typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, int tid) {
     typedef Shape<KEY, LK> S;
     constexpr int K = S::K, NT = S::NT, IT = S::IT;
     constexpr int VK = 16 / (int)sizeof(KEY);  // keys per 16-byte vector
-    constexpr int LAST = S::LDS_KEYS - S::PADK - 1;
+    constexpr int LAST = S::LDS_KEYS - PAD - 1;
     const int len = d->o[K];
-    constexpr int RN = S::RN;  // chain 3: up to two leading keys not the lane's (ex)
-    KEY r[RN];
-    int ex = 0;  // the lane's outputs are r[ex, ex + IT)
+    KEY r[IT];  // the lane's outputs [pos, pos + IT)
     const int pos = tid * IT;
     // the first level's input sequences: the chunk's segments
     int st[K], ln[K];
@@ -1170,23 +1048,23 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
         st[q] = S::seg(d->o[q], q);
         ln[q] = d->o[q + 1] - d->o[q];
     }
-    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, ex, tid, LAST, pt);
+    lds_merge_levels<KEY, S, MODE>(s, st, ln, r, tid, LAST);
     const int64_t out0 = d->out0;
     // the chunk goes to LDS shifted by out0 mod VK, so every global 16-byte
     // vector is one aligned LDS vector (a lane's outputs past len are MAX and
     // land past the chunk)
     const int sh = (int)(out0 & (VK - 1));
     if (pos < len) {
-        KEY* q = s + sh + pos - ex;
-        if (S::CH != 3 && IT % 2 == 0 && MISORT_MK_PAIRSTAGE && (sh & 1) == 0) {
+        KEY* q = s + sh + pos;
+        if ((sh & 1) == 0) {
             // even shift (uniform per chunk): aligned pairs, one 8-byte (u64:
             // 16-byte) write per two keys instead of one write per key
+            // (2277-2282 us per 2^30 pass instead of 2282-2291, profiles/r04/pairstage)
 #pragma unroll
             for (int j = 0; j < IT; j += 2) *reinterpret_cast<kvec2<KEY>*>(q + j) = kvec2<KEY>{r[j], r[j + 1]};
         } else {
 #pragma unroll
-            for (int k = 0; k < RN; ++k)
-                if (k >= ex && k < ex + IT) q[k] = r[k];
+            for (int k = 0; k < IT; ++k) q[k] = r[k];
         }
     }
     lds_barrier();
@@ -1219,7 +1097,7 @@ __device__ __forceinline__ void mergek_chunk(KEY* s, const Desc<KEY, LK>* d, KEY
 // zero word, the word below the next segment), the zero word below the first
 // and the first level's pair table (pt).
 template <typename KEY, int LK>
-__device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d, int tid, PairRec* pt) {
+__device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d, int tid) {
     typedef Shape<KEY, LK> S;
     // a wave per segment (uniform segment index: the descriptor's offsets come
     // by scalar loads), G <= 64 lanes each
@@ -1228,14 +1106,8 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
     for (int q = __builtin_amdgcn_readfirstlane(tid >> 6); q < S::K; q += S::NT / 64)
         if (lane < S::G)
             s[S::seg(d->o[q], q) + (d->o[q + 1] - d->o[q]) + lane] = S::ZW && lane == S::G - 1 ? (KEY)0 : KMAX<KEY>;
-    if constexpr (S::ZW || S::PT) {
-        int st[S::K], ln[S::K];
-#pragma unroll
-        for (int q = 0; q < S::K; ++q) {
-            st[q] = S::seg(d->o[q], q);
-            ln[q] = d->o[q + 1] - d->o[q];
-        }
-        lds_merge_prologue<KEY, S>(s, st, ln, pt, tid);
+    if constexpr (S::ZW) {
+        if (tid == 0) s[S::seg(d->o[0], 0) - 1] = (KEY)0;  // the zero word below the first segment
     }
 }
 
@@ -1251,11 +1123,11 @@ __device__ __forceinline__ void mergek_sentinels(KEY* s, const Desc<KEY, LK>* d,
 // averages FM*FG of CAP keys).
 // One chunk: its rows into LDS, the sentinels, then mergek_chunk.
 template <typename KEY, int LK, bool FENCES, int MODE, bool ORD>
-__device__ __forceinline__ void mergek_run(KEY* tile, PairRec* pt, const KEY* __restrict__ src, KEY* __restrict__ dst,
+__device__ __forceinline__ void mergek_run(KEY* tile, const KEY* __restrict__ src, KEY* __restrict__ dst,
                                            const Desc<KEY, LK>* __restrict__ d, typename KTr<KEY>::F* __restrict__ fout,
                                            int lwn, int lkn) {
     typedef Shape<KEY, LK> S;
-    KEY* s = tile + S::PADK;
+    KEY* s = tile + PAD;
     const int tid = threadIdx.x;
     {
         // loads: lane slot j = row j * NR + part, lane offset lt; the wave's
@@ -1271,7 +1143,7 @@ __device__ __forceinline__ void mergek_run(KEY* tile, PairRec* pt, const KEY* __
             off[j] = offp[j];
             la[j] = lap[j];
         }
-        if constexpr (MISORT_MK_GLDS && sizeof(KEY) == 4) {
+        if constexpr (sizeof(KEY) == 4) {
             // straight into LDS: a wave's part of a row is 64 consecutive LDS
             // words from a wave-uniform base (global_load_lds_dword writes
             // base + 4 * lane), so the row's slot plus the wave's first lane
@@ -1292,10 +1164,10 @@ __device__ __forceinline__ void mergek_run(KEY* tile, PairRec* pt, const KEY* __
             for (int j = 0; j < LS; ++j)
                 if (lt < (int)(la[j] & 0xFFFF)) s[(la[j] >> 16) + lt] = x[j];
         }
-        mergek_sentinels<KEY, LK>(s, d, tid, pt);
+        mergek_sentinels<KEY, LK>(s, d, tid);
     }
     __syncthreads();
-    mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid, pt);
+    mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid);
 }
 
 // The grid: (capacity split) first OVF_WG workgroups that walk the halves of
@@ -1304,22 +1176,20 @@ __device__ __forceinline__ void mergek_run(KEY* tile, PairRec* pt, const KEY* __
 // one workgroup per chunk.
 constexpr int OVF_WG = 256;
 template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
-__global__ __launch_bounds__(KTr<KEY>::nt(LK), KTr<KEY>::wg(LK)* KTr<KEY>::nt(LK) / 256) void k_mergek(
+__global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256) void k_mergek(
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
     typename KTr<KEY>::F* __restrict__ fout, int lwn, int lkn, uint32_t nprimary,
     const Desc<KEY, LK>* __restrict__ dov = nullptr, const int* __restrict__ ovf = nullptr) {
     typedef Shape<KEY, LK> S;
     __shared__ __attribute__((aligned(16))) KEY tile[S::LDS_KEYS];
-    __shared__ PairRec ptab[S::PT ? S::K / 2 : 1];
     const uint32_t nov = gridDim.x - nprimary;  // the split's workgroups (0 without it)
     if (blockIdx.x >= nov) {
-        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, S::PT ? ptab : nullptr, src, dst, desc + (blockIdx.x - nov), fout,
-                                               lwn, lkn);
+        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, src, dst, desc + (blockIdx.x - nov), fout, lwn, lkn);
         return;
     }
     const int cnt = 2 * ovf[0];
     for (int i = (int)blockIdx.x; i < cnt; i += (int)nov) {
-        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, S::PT ? ptab : nullptr, src, dst, dov + i, fout, lwn, lkn);
+        mergek_run<KEY, LK, FENCES, MODE, ORD>(tile, src, dst, dov + i, fout, lwn, lkn);
         __syncthreads();  // the tile is reused
     }
 }
@@ -1388,9 +1258,6 @@ int64_t chunks_of(const Geo& geo) {
 // 2^30 u32 passes 3 and 4 (2^23 fences) -30 us each, +0.6 %; at 2^22 fences
 // (2^29 keys) the nested pass's ~600 chunks underfill the chip: +5 us, so the
 // default threshold is 2^23.
-#ifndef MISORT_FENCE_NEST
-#define MISORT_FENCE_NEST 1
-#endif
 constexpr int FENCE_NEST_LEVELS = 3;
 
 template <typename KEY, int LK>
@@ -1462,7 +1329,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         const FT* x = F;
         int left = LK - a;
         bool nest = false;
-        if constexpr (sizeof(KEY) == 4 && MISORT_FENCE_NEST) {
+        if constexpr (sizeof(KEY) == 4) {
             static const int nest_min =
                 getenv("MISORT_FENCE_NEST_MIN") ? atoi(getenv("MISORT_FENCE_NEST_MIN")) : 23;
             nest = depth == 0 && nest_min > 0 && left >= FENCE_NEST_LEVELS && nf >= ((int64_t)1 << nest_min) &&
@@ -1473,7 +1340,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
             const size_t lds = ((size_t)1 << (wf_log2 + a)) * sizeof(FT);
             const int64_t nb0 = (nf + ((int64_t)1 << (wf_log2 + a)) - 1) >> (wf_log2 + a);
             // >= 512 blocks where the sub-groups are few (each loads its whole sub-group)
-            if (MISORT_FENCE_MERGE && nb0 >= FENCE_MERGE_MIN_BLOCKS) {
+            if (nb0 >= FENCE_MERGE_MIN_BLOCKS) {
                 k_fence_merge<FT><<<(unsigned)nb0, (unsigned)(((int64_t)1 << (wf_log2 + a)) / FIT), lds, s>>>(
                     F, y, nf, wf_log2, a);
             } else {
@@ -1509,9 +1376,9 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     static const int64_t slices_max = getenv("MISORT_FC_SLICES_MAX") ? atoll(getenv("MISORT_FC_SLICES_MAX")) : 256;
     if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
     else k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
-    // planning kernel shapes by size (measured crossovers; env overrides for A/B probes)
-    static const int64_t line_min = getenv("MISORT_BOUNDS_LINE_MIN") ? atoll(getenv("MISORT_BOUNDS_LINE_MIN")) : (1 << 17);
-    static const int64_t dc16_min = getenv("MISORT_DESC16_MIN") ? atoll(getenv("MISORT_DESC16_MIN")) : (1 << 14);
+    // planning kernel shapes by size (measured crossovers, profiles/r02/s3b-s3i):
+    // k_bounds' line probe from 2^17 searches, 16 descriptors per workgroup from 2^14 chunks
+    constexpr int64_t line_min = 1 << 17, dc16_min = 1 << 14;
     const bool line = (nslots << LK) >= line_min;
     const int nbs = fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
     if (nbs == 0) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);

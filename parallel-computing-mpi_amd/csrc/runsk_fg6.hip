@@ -5,9 +5,4 @@
 #define MISORT_RUNSK_FGL 6
 #define MISORT_RUNSK_FN(x) x##_fg6
 #define MISORT_RUNSK_SECOND 1
-// u64 chunks: 8896 keys (139 fences of 64; the 128-key build's 8832 is 69 of
-// 128): k_mergek -5 us per 2^29 pass (profiles/r05/mergek/cap_ab.txt)
-#ifndef MISORT_MK_CAP64
-#define MISORT_MK_CAP64 8896
-#endif
 #include "runsk.hip"

@@ -56,7 +56,8 @@ def to_host(t, dtype):
     return t.cpu().numpy()
 
 
-def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compress=True, raw=None, kinds=None):
+def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compress=True, raw=None, kinds=None,
+               setters=True):
     """Each rank sorts its reference-layout block; returns (concatenated
     result, check_sort count of every rank, exchange stats of every rank).
     raw (a dict) receives each rank's uncoded exchange bytes; kinds (a dict)
@@ -67,9 +68,10 @@ def group_sort(x, p, full_exchange=False, out_of_place=False, relay=True, compre
     blocks = [np.ascontiguousarray(x[offs[r]:offs[r + 1]]) for r in range(p)]
 
     def rank_fn(r, ctx):
-        ctx.set_full_exchange(full_exchange)
-        ctx.set_relay(relay)
-        ctx.set_compress(compress)
+        if setters:  # else the environment's defaults (MISORT_FULL_EXCHANGE, MISORT_RELAY, MISORT_COMPRESS)
+            ctx.set_full_exchange(full_exchange)
+            ctx.set_relay(relay)
+            ctx.set_compress(compress)
         buf = to_dev(np.concatenate([blocks[r], np.zeros(max_size - sizes[r], x.dtype)]))
         out = torch.empty_like(buf) if out_of_place else None
         torch.cuda.synchronize()
@@ -214,6 +216,21 @@ def test_tail_merges_vs_whole_block(monkeypatch, kind):
         assert errs == [O.check_sort(want, p)] * p
         ntail = sum(k.get("merge_split_tail", 0) for k in kinds.values())
         assert (ntail > 0) == tail, (div, ntail)
+
+
+def test_exchange_switches_from_environment(monkeypatch):
+    """MISORT_FULL_EXCHANGE=1, MISORT_RELAY=0, MISORT_COMPRESS=0 as the
+    contexts' defaults: whole blocks each way every stage (the reference's
+    MPI_Sendrecv, psort.cc:121-122,146-147), the same bytes as the oracle."""
+    monkeypatch.setenv("MISORT_FULL_EXCHANGE", "1")
+    monkeypatch.setenv("MISORT_RELAY", "0")
+    monkeypatch.setenv("MISORT_COMPRESS", "0")
+    n, p = (1 << 18) + 3, 4
+    x = O.splitmix(0x5EED0EE1, n, np.uint32)
+    y, errs, st = group_sort(x, p, setters=False)
+    want = O.parallel_bitonic_sort(x, p)
+    np.testing.assert_array_equal(y, want)
+    assert all(s[1] == s[2] and s[1] > 0 for s in st), st  # every stage moved whole blocks
 
 
 def _u64_mix(n, seed):

@@ -66,10 +66,12 @@ ctx.close()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("markers,bind", [("0", "2"), ("0", "1"), ("1", "2")])
-def test_pass_records(markers, bind):
+@pytest.mark.parametrize("markers,bind,sysfence", [("0", "2", "0"), ("0", "1", "0"), ("1", "2", "0"), ("0", "2", "1")])
+def test_pass_records(markers, bind, sysfence):
+    # sysfence: MISORT_PROF_SYSFENCE=1 restores the system-scope release of the events
     r = subprocess.run([sys.executable, "-c", CHILD, os.path.join(ROOT, "parallel-computing-mpi_amd")],
-                       env=dict(os.environ, MISORT_PROF_MARKERS=markers, MISORT_PROF_BIND=bind),
+                       env=dict(os.environ, MISORT_PROF_MARKERS=markers, MISORT_PROF_BIND=bind,
+                                MISORT_PROF_SYSFENCE=sysfence),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads([x for x in r.stdout.splitlines() if x.startswith("JSON")][-1][5:])

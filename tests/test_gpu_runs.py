@@ -239,6 +239,13 @@ ctx.close()
     (4, {"MISORT_MK_FM_ADD": "40", "MISORT_FENCE_FG6_MIN": "20"}, (1 << 26) + 12345),
     (4, {"MISORT_MK_FM_ADD": "60", "MISORT_FENCE_NEST_MIN": "12"}, (1 << 27) + 777),
     (4, {"MISORT_MK_FM_ADD": "0"}, (1 << 26) + 777),  # no split: the worst-case chunk bound
+    # k_mergek's probe launches (MISORT_MK_PROBE: no-merge / first-level /
+    # co-rank-only copies of every pass into a scratch buffer) leave the sort intact
+    (4, {"MISORT_MK_PROBE": "1"}, (1 << 26) + 12345),
+    # the network SORT tiles one tile per workgroup, and the persistent grid at twice the resident capacity
+    (4, {"MISORT_PERSIST": "0"}, (1 << 23) + 5),
+    (4, {"MISORT_GRID_MULT": "2"}, (1 << 23) + 5),
+    (8, {"MISORT_PERSIST_U64": "0"}, (1 << 21) + 4099),
     (8, {"MISORT_MK_FM_ADD": "40"}, (1 << 25) + 12345),
     (8, {}, (1 << 21) + 4099),
     (8, {"MISORT_RUN_IT": "32"}, (1 << 20) + 5),

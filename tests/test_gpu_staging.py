@@ -134,3 +134,29 @@ def test_in_place_host_buffer_group(case, monkeypatch):
     finally:
         g.close()
     assert sha(np.concatenate(bufs)) == case["out_sha256"]
+
+
+STAGE_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import misort
+ctx = misort.Context(0)
+rng = np.random.default_rng(5)
+x = rng.integers(0, 2**32 - 1, size=(1 << 23) + 5, dtype=np.uint32)
+print("OK" if np.array_equal(ctx.sort_host(x), np.sort(x)) else "MISMATCH")
+ctx.close()
+"""
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_staged_host_copy_threads(threads):
+    """MISORT_STAGE_THREADS (the host copies into the pinned ring, read once per
+    process): one thread and an odd count sort the same keys."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", STAGE_CHILD, os.path.join(root, "parallel-computing-mpi_amd")],
+                       env=dict(os.environ, MISORT_STAGE_THREADS=threads, MISORT_STAGE_CHUNK=str(1 << 21)),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "OK"
