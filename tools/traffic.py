@@ -48,7 +48,7 @@ def kernel_shape(name):
         return "v16"
     if "k_mergek" in name:
         return "v8" if u64 else "lds4"
-    if "k_bounds" in name or "k_chunk_desc" in name:
+    if "k_bounds" in name or "k_chunk_desc" in name or "k_split_desc" in name:
         return "line128"
     if "k_runs_partition" in name or "k_fence_gather" in name:
         return "probe4"
@@ -90,7 +90,7 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
             # u32 sorts: k_mergek on unsigned long is a pass's nested fence
             # merge (runsk.hip MISORT_FENCE_NEST), planning of that pass
             fam = "runk_plan" if U32 and "k_mergek<unsigned long" in name else "run_mergek_kernel"
-        elif re.search(r"k_fence_gather|k_fence_lds|k_fence_merge|k_fence_counts|k_scan_totals|k_bounds|k_chunk_desc",
+        elif re.search(r"k_fence_gather|k_fence_lds|k_fence_merge|k_fence_counts|k_scan_totals|k_bounds|k_chunk_desc|k_split_desc",
                        name):
             fam = "runk_plan"
         else:
