@@ -175,7 +175,7 @@ void* mergek_fence_buffer_fg6(int64_t n, int key_bytes, int phase, hipStream_t s
 void mergek_release_fg6(hipStream_t s);
 int mergek_take_error_fg6(hipStream_t s);
 // The fence stride (log2 keys) the local sort of n keys uses: 6 (runsk_fg6)
-// from 2^MISORT_FENCE_FG6_MIN keys (u32: 30, u64: 29), else MERGEK_FENCE_LOG2.
+// from 2^MISORT_FENCE_FG6_MIN keys (u32: never by default, u64: 29), else MERGEK_FENCE_LOG2.
 int mergek_fence_log2(int64_t n, int key_bytes);
 int merge_levelk_lw_min(int key_bytes);   // shortest input runs (log2) of a multi-way pass
 int merge_levelk_lwk_max(int key_bytes);  // largest output runs (log2)

@@ -155,11 +155,9 @@ def main():
             mb = (2 * x["n_me"] + k) * w
             if k * a.tail_div <= x["n_me"]:
                 # the runtime's small-bracket path: in place at the block's end
-                # (merge_split_tail); the block is restored before each rep
-                os.environ["MISORT_MERGE_SPLIT_TAIL"] = "1"
-                t = timed(lambda: ctx.compare_split(mo, x["recv"], x["keep_max"], out=mo),
+                # (misort_merge_split_tail); the block is restored before each rep
+                t = timed(lambda: ctx.compare_split(mo, x["recv"], x["keep_max"], out=mo, in_place_tail=True),
                           setup=lambda: mo.copy_(x["mine"]))
-                os.environ.pop("MISORT_MERGE_SPLIT_TAIL")
                 mine, rv = x["mine"], x["recv"]
                 if x["keep_max"]:
                     win = int(torch.searchsorted(mine, rv[-1:], right=True).item())
