@@ -560,6 +560,87 @@ __global__ __launch_bounds__(512) void k_scan_totals(int* __restrict__ bsum, int
     }
 }
 
+// Small sorts (fused planning, runs of <= 2^MISORT_FENCE_RANK_MAX fences): the
+// group's fences into total order AND the per-chunk fence counts in ONE launch,
+// in place of the fence merge levels (k_fence_lds / k_fence_merge and global
+// merge levels) and k_fence_counts -- at these sizes each of those launches is
+// latency-bound.  A thread per fence: its rank in the group = its index in its
+// run + its lower bound in each other run (K - 1 power-of-two searches over
+// the run's fence list, stepping together so their loads overlap; lanes of a
+// wave hold neighbouring fences of one run, so they probe the same or
+// adjacent lines).  Counts: chunk t starts at merged fence t * fm, and run q's
+// fences before it are the i with rank(q, i) < t * fm, so fence i of run q
+// (rank p, its predecessor's rank p') writes i for every t with p' < t * fm <=
+// p, and the run's last fence writes i + 1 for the chunks after it -- every
+// (chunk, run) entry once, as absolute counts (the block totals bsum are
+// zeroed: no scan).  Block b owns fences [b (RANK_NT - 1), (b + 1) (RANK_NT -
+// 1)); its thread 0 ranks the fence before them (the predecessor of thread 1's).
+constexpr int RANK_NT = 256;
+template <typename FT, int LK>
+__global__ __launch_bounds__(RANK_NT) void k_fence_rank(const FT* __restrict__ F, FT* __restrict__ M, Geo geo,
+                                                        int64_t nf, int wf_log2, int* __restrict__ P,
+                                                        int* __restrict__ bsum, int64_t nbsum) {
+    constexpr int K = 1 << LK;
+    __shared__ int sp[RANK_NT];
+    const int tid = threadIdx.x;
+    for (int64_t j = (int64_t)blockIdx.x * RANK_NT + tid; j < nbsum; j += (int64_t)gridDim.x * RANK_NT) bsum[j] = 0;
+    const int64_t e = (int64_t)blockIdx.x * (RANK_NT - 1) - 1 + tid;
+    const bool valid = e >= 0 && e < nf;
+    const int gl = wf_log2 + LK, wf = 1 << wf_log2;
+    int64_t g = 0, gbase = 0;
+    int nfg = 0, q = 0, i = 0, p = -1;
+    if (valid) {
+        g = e >> gl;
+        gbase = g << gl;
+        nfg = nf - gbase < ((int64_t)1 << gl) ? (int)(nf - gbase) : 1 << gl;
+        const int gi = (int)(e - gbase);
+        q = gi >> wf_log2;
+        i = gi & (wf - 1);
+        const FT v = F[e];
+        int pos[K], len[K];
+        const FT* fr[K];  // run r's fences (a run with none, or q itself: fence e, never taken)
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int l = nfg - r * wf;
+            len[r] = r == q ? 0 : (l <= 0 ? 0 : (l < wf ? l : wf));
+            pos[r] = 0;
+            fr[r] = len[r] > 0 ? F + gbase + ((int64_t)r << wf_log2) : F + e;
+        }
+        // unconditional loads at clamped probes (a guarded load per run made
+        // each wait for the last), then the steps taken
+        for (int st = wf; st > 0; st >>= 1) {
+            FT x[K];
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                const int j = pos[r] + st < len[r] ? pos[r] + st : len[r];
+                x[r] = fr[r][j > 0 ? j - 1 : 0];
+            }
+#pragma unroll
+            for (int r = 0; r < K; ++r) pos[r] += pos[r] + st <= len[r] && x[r] < v ? st : 0;
+        }
+        p = i;
+#pragma unroll
+        for (int r = 0; r < K; ++r) p += pos[r];
+        M[gbase + p] = v;
+    }
+    sp[tid] = p;
+    __syncthreads();
+    if (!valid || tid == 0) return;
+    const uint32_t fm = (uint32_t)geo.fm;
+    const int64_t c0 = g * geo.kf;  // the group's first chunk (the tail group's too)
+    const int nch = (int)geo.nchunks(g);
+    const int lq = nfg - q * wf < wf ? nfg - q * wf : wf;  // run q's fences in the group
+    const int t0 = i == 0 ? 0 : (int)((uint32_t)sp[tid - 1] / fm) + 1;  // thread tid - 1 holds fence e - 1
+    const int t1 = (int)((uint32_t)p / fm);
+    for (int t = t0; t <= t1; ++t) P[(c0 + t) * K + q] = i;
+    if (i == lq - 1)
+        for (int t = t1 + 1; t < nch; ++t) P[(c0 + t) * K + q] = i + 1;
+    // runs with no fences in this group (a tail group): zero counts
+    const int gi = (int)(e - gbase), nruns = (nfg + wf - 1) >> wf_log2;
+    if (gi < nch)
+        for (int r = nruns; r < K; ++r) P[(c0 + gi) * K + r] = 0;
+}
+
 // Interpolated guess of where v falls between positions a and b whose keys
 // are ka < kb.
 template <typename KEY>
@@ -1319,7 +1400,14 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     int* ovf = split ? (int*)(base + 2 * fb + bb + cb + sb + db) : nullptr;  // [count, chunks...]
     if (gather) k_fence_gather<KEY><<<(unsigned)((nf + 255) / 256), 256, 0, s>>>(src, n, lw, LK, F);
     const int wf_log2 = lw - FG_LOG2;  // fences per run = 2^wf_log2
-    {
+    // MISORT_FENCE_RANK_MAX: fused passes whose runs hold <= 2^this fences rank
+    // them and count them in one launch (k_fence_rank); 0 = never
+    static const int rank_max = getenv("MISORT_FENCE_RANK_MAX") ? atoi(getenv("MISORT_FENCE_RANK_MAX")) : 14;
+    const bool rank = fuse && wf_log2 <= rank_max;
+    if (rank) {
+        k_fence_rank<FT, LK><<<(unsigned)((nf + RANK_NT - 2) / (RANK_NT - 1)), RANK_NT, 0, s>>>(
+            F, M, geo, nf, wf_log2, cnt, bsum, nbk * S::K);
+    } else {
         // the group's fences into total order, landing in M: the first a levels
         // in LDS (sub-groups of 2^a runs, <= 64 KiB of fences), the other
         // LK - a as fence merge levels (runs of >= 2^FL fences), ping-ponging
@@ -1374,14 +1462,18 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // few blocks: per-lane slices; many: coalesced atomics (k_fence_counts)
     // MISORT_FC_SLICES_MAX (tests): the block count from which the coalesced form counts
     static const int64_t slices_max = getenv("MISORT_FC_SLICES_MAX") ? atoll(getenv("MISORT_FC_SLICES_MAX")) : 256;
-    if (nb < slices_max) k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
-    else k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
+    if (rank) {
+    } else if (nb < slices_max) {
+        k_fence_counts<FT, true><<<(unsigned)nb, COUNT_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
+    } else {
+        k_fence_counts<FT, false><<<(unsigned)nb, FC_NT, 0, s>>>(M, geo, nchunks, cpb, cnt, bsum, ovf);
+    }
     // planning kernel shapes by size (measured crossovers, profiles/r02/s3b-s3i):
     // k_bounds' line probe from 2^17 searches, 16 descriptors per workgroup from 2^14 chunks
     constexpr int64_t line_min = 1 << 17, dc16_min = 1 << 14;
     const bool line = (nslots << LK) >= line_min;
-    const int nbs = fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
-    if (nbs == 0) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
+    const int nbs = !rank && fuse && plan_scan && nb * S::K <= PLAN_SCAN_MAX ? (int)nb : 0;
+    if (nbs == 0 && !rank) k_scan_totals<<<1, 64 * ((S::K + 1) / 2), 0, s>>>(bsum, nb, S::K);
     if (!fuse)
         k_bounds<KEY><<<(unsigned)(((nslots << LK) + 255) / 256), 256, 0, s>>>(src, F, M, cnt, bsum, cpb, geo,
                                                                               nslots, bounds, line);

@@ -212,9 +212,14 @@ ctx.close()
     (4, {}, (1 << 16) + 3),
     (4, {"MISORT_RUN_FUSE": "0", "MISORT_PLAN_FUSE": "0"}, (1 << 24) + 999),  # k_runs_partition, k_bounds
     (4, {"MISORT_PLAN_FUSE": "2"}, (1 << 26) + 12345),  # bounds inside k_chunk_desc<16>
-    (4, {"MISORT_PLAN_SCAN": "0"}, (1 << 23) + 77),  # fused bounds, block totals by k_scan_totals
-    (4, {"MISORT_FC_SLICES_MAX": "0"}, (1 << 23) + 77),  # fence counts by the coalesced (large-sort) form
-    (8, {"MISORT_FC_SLICES_MAX": "0"}, (1 << 22) + 3),
+    (4, {"MISORT_PLAN_SCAN": "0", "MISORT_FENCE_RANK_MAX": "0"}, (1 << 23) + 77),  # fused bounds, k_scan_totals
+    # fence ranks and counts in one launch (k_fence_rank; the default for fused
+    # passes of <= 2^14 fences per run): off, and forced on larger runs
+    (4, {"MISORT_FENCE_RANK_MAX": "0"}, (1 << 24) + 999),
+    (4, {"MISORT_FENCE_RANK_MAX": "20", "MISORT_PLAN_FUSE": "2"}, (1 << 26) + 12345),
+    (8, {"MISORT_FENCE_RANK_MAX": "20", "MISORT_PLAN_FUSE": "2"}, (1 << 25) + 12345),
+    (4, {"MISORT_FC_SLICES_MAX": "0", "MISORT_FENCE_RANK_MAX": "0"}, (1 << 23) + 77),  # coalesced fence counts
+    (8, {"MISORT_FC_SLICES_MAX": "0", "MISORT_FENCE_RANK_MAX": "0"}, (1 << 22) + 3),
     (4, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),  # every 2-way level fused
     # fence merges as one nested u64 multi-way pass (the default from 2^22
     # fences, i.e. 2^29 keys): 4 levels, 3 + 3 levels, 8-way passes

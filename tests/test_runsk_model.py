@@ -151,3 +151,96 @@ def test_chunks_tile_and_bound(lk, lw, n_groups, tail, kind):
             merged.append(chunk)
         want = np.sort(x[base: base + sum(lens)])
         np.testing.assert_array_equal(np.concatenate(merged), want)
+
+
+def fence_rank_model(F, nf, wf_log2, lk, fm, nt=256):
+    """k_fence_rank (runsk.hip) on a flat fence array: blocks of nt threads own
+    nt - 1 fences each (thread 0 ranks the fence before them); returns the
+    merged fences M and the per-(chunk, run) counts P exactly as the kernel
+    writes them (-1 = never written)."""
+    K, wf, gl = 1 << lk, 1 << wf_log2, wf_log2 + lk
+    ngroups = (nf + (1 << gl) - 1) >> gl
+    fences_per_group = 1 << gl
+    kf = (fences_per_group + fm - 1) // fm
+    nch_of = [kf if (g + 1) << gl <= nf else (min(nf - (g << gl), fences_per_group) + fm - 1) // fm
+              for g in range(ngroups)]
+    M = np.zeros(nf, np.uint64)
+    P = np.full((ngroups * kf + 1) * K, -1, np.int64)
+    nblocks = (nf + nt - 2) // (nt - 1)
+    for b in range(nblocks):
+        sp = [-1] * nt
+        info = [None] * nt
+        for tid in range(nt):
+            e = b * (nt - 1) - 1 + tid
+            if e < 0 or e >= nf:
+                continue
+            g = e >> gl
+            gbase = g << gl
+            nfg = min(nf - gbase, 1 << gl)
+            gi = e - gbase
+            q, i = gi >> wf_log2, gi & (wf - 1)
+            v = F[e]
+            p = i
+            for r in range(K):
+                ln = 0 if r == q else max(0, min(nfg - r * wf, wf))
+                pos, st = 0, wf
+                while st > 0:  # the kernel's power-of-two lower bound
+                    if pos + st <= ln and F[gbase + r * wf + pos + st - 1] < v:
+                        pos += st
+                    st >>= 1
+                p += pos
+            M[gbase + p] = v
+            sp[tid] = p
+            info[tid] = (g, gbase, nfg, gi, q, i, p)
+        for tid in range(1, nt):
+            if info[tid] is None:
+                continue
+            g, gbase, nfg, gi, q, i, p = info[tid]
+            c0, nch = g * kf, nch_of[g]
+            lq = min(nfg - q * wf, wf)
+            t0 = 0 if i == 0 else sp[tid - 1] // fm + 1
+            t1 = p // fm
+            for t in range(t0, t1 + 1):
+                P[(c0 + t) * K + q] = i
+            if i == lq - 1:
+                for t in range(t1 + 1, nch):
+                    P[(c0 + t) * K + q] = i + 1
+            nruns = (nfg + wf - 1) >> wf_log2
+            if gi < nch:
+                for r in range(nruns, K):
+                    P[(c0 + gi) * K + r] = 0
+    return M, P, nch_of, kf
+
+
+@pytest.mark.parametrize("lk,wf_log2,nf,fm", [(3, 5, 3 * 256 + 40, 7), (3, 5, 256 * 2, 60), (2, 6, 256 + 64 * 2 + 3, 9),
+                                              (4, 3, 16 * 8 * 3 + 17, 5), (1, 7, 700, 13), (3, 8, 2048 + 1, 66)])
+@pytest.mark.parametrize("kind", ["uniform", "dup", "interleaved"])
+def test_fence_rank_counts(lk, wf_log2, nf, fm, kind):
+    """k_fence_rank's merged order and counts equal the sorted group fences and
+    the direct per-(chunk, run) counts, tail groups with short and missing runs
+    included."""
+    K, wf, gl = 1 << lk, 1 << wf_log2, wf_log2 + lk
+    rng = np.random.default_rng(nf + fm)
+    if kind == "uniform":
+        keys = rng.integers(0, 2**20, nf)
+    elif kind == "dup":
+        keys = rng.integers(0, 3, nf)
+    else:
+        keys = np.arange(nf) % wf * K + (np.arange(nf) // wf) % K
+    F = np.zeros(nf, np.uint64)
+    for s in range(0, nf, wf):  # per run: sorted keys packed with (run, position) as the fences are
+        e = np.arange(s, min(s + wf, nf))
+        run = (e >> wf_log2) & (K - 1)
+        F[s:s + e.size] = ((np.sort(keys[s:s + e.size]).astype(np.uint64) << np.uint64(32))
+                           | (run.astype(np.uint64) << np.uint64(32 - lk)) | (e & (wf - 1)).astype(np.uint64))
+    M, P, nch_of, kf = fence_rank_model(F, nf, wf_log2, lk, fm)
+    for g in range(len(nch_of)):
+        gbase = g << gl
+        nfg = min(nf - gbase, 1 << gl)
+        want = np.sort(F[gbase:gbase + nfg])
+        np.testing.assert_array_equal(M[gbase:gbase + nfg], want)
+        for t in range(nch_of[g]):
+            start = int(want[t * fm])
+            for r in range(K):
+                run = F[gbase + r * wf: gbase + min(nfg, (r + 1) * wf)] if r * wf < nfg else F[:0]
+                assert P[(g * kf + t) * K + r] == int(np.sum(run < start)), (g, t, r)
