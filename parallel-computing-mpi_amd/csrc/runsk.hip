@@ -607,7 +607,10 @@ __global__ __launch_bounds__(RANK_NT) void k_fence_rank(const FT* __restrict__ F
             fr[r] = len[r] > 0 ? F + gbase + ((int64_t)r << wf_log2) : F + e;
         }
         // unconditional loads at clamped probes (a guarded load per run made
-        // each wait for the last), then the steps taken
+        // each wait for the last), then the steps taken.  The searches are
+        // bound by load issue: a radix-4 search (3x the loads in half the
+        // rounds) ran 1.6x slower, and loads of the key halves only over the
+        // K - 1 other runs 1.25x slower (profiles/r06/plan/rank_ab.txt)
         for (int st = wf; st > 0; st >>= 1) {
             FT x[K];
 #pragma unroll
