@@ -123,6 +123,17 @@ def main():
     torch.cuda.synchronize()
 
     def timed(fn, setup=None):
+        if setup is None:
+            # back to back between one pair of events: device time, not the
+            # host's launch latency of one op (a sort is ~40 launches)
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(a.reps):
+                fn()
+            e1.record(s)
+            e1.synchronize()
+            return e0.elapsed_time(e1) / a.reps
         ms = []
         for _ in range(a.reps + 1):
             if setup:
