@@ -260,6 +260,23 @@ int split_fm_add() {
     return fm > fm0 ? fm - fm0 : 0;
 }
 
+// A group whose fence count lies just above a multiple of fm ends in a nearly
+// empty chunk (2^30 u32 pass 1: 2048 fences a group, fm 93 -> 23 chunks, the
+// last of 2 fences): up to FM_BALANCE fences more per chunk when that saves
+// the group a chunk, within the split's bound (halves fit, 8-bit counts), and
+// only where that chunk is >= 1/BAL_NC_MAX of the group's: 2^30 +0.35 %; on
+// every pass (+1 fence a chunk, more splits for 1 chunk in 250) 2^27 -1 %
+// (profiles/r06/mergek/balance_ab.txt).
+constexpr int FM_BALANCE = 3, BAL_NC_MAX = 32;
+template <typename KEY, int LK>
+int balance_fm(int fm, int64_t gf) {
+    const int K = 1 << LK, cap = KTr<KEY>::cap(LK);
+    const int64_t nc = gf / fm;
+    if (nc < 1 || nc > BAL_NC_MAX || nc * fm == gf) return fm;
+    const int fm2 = (int)((gf + nc - 1) / nc);
+    return fm2 <= fm + FM_BALANCE && fm2 <= 255 && ((fm2 + 1) / 2 + K) * (int)FG <= cap ? fm2 : fm;
+}
+
 // F[i] = fence of position i*FG (the first multi-way pass after the SORT tile).
 template <typename KEY>
 __global__ void k_fence_gather(const KEY* __restrict__ src, int64_t n, int lw, int lk,
@@ -1365,7 +1382,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     // extra workgroups run the halves).  A half holds at most ceil(fm / 2) + K fences'
     // worth of keys, so fm stays within 2 (CAP / FG - K) (and 8-bit counts).
     const int fma = fuse ? 0 : split_fm_add<KEY, LK>();
-    if (fma > 0) geo = make_geo<KEY>(n, lw, LK, geo.fm + fma);
+    if (fma > 0) geo = make_geo<KEY>(n, lw, LK, balance_fm<KEY, LK>(geo.fm + fma, ((int64_t)1 << (lw + LK)) >> FG_LOG2));
     const bool split = fma > 0;
     const bool tail = (geo.nfull << (lw + LK)) < n;
     const int64_t nchunks = chunks_of(geo);
