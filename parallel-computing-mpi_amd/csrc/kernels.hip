@@ -79,6 +79,38 @@ __device__ int64_t corank(const K* A, int64_t na, const K* B, int64_t nb, int64_
     return lo;
 }
 
+// The same by a radix-R lifting search: R - 1 probes per round (their loads in
+// flight together), log_R of the bisection's dependent rounds -- the partition
+// of a whole-block merge-split is latency-bound (one thread per 2048-output
+// tile, 27 rounds at 2^27 + 2^26 keys).
+template <int R, typename K>
+__device__ int64_t corank_r(const K* A, int64_t na, const K* B, int64_t nb, int64_t d) {
+    const int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    if (lo >= hi) return lo;
+    int64_t st = 1;
+    while (st * R <= hi - lo) st *= R;
+    int64_t base = lo;  // A[i] <= B[d - 1 - i] holds for every i < base
+    for (; st > 0; st /= R) {
+        K a[R - 1], b[R - 1];
+#pragma unroll
+        for (int u = 0; u < R - 1; ++u) {
+            const int64_t i = base + (u + 1) * st - 1;
+            const int64_t ic = i < hi ? i : hi - 1;  // clamped: never taken
+            a[u] = A[ic];
+            b[u] = B[d - 1 - ic];
+        }
+        int64_t add = 0;
+#pragma unroll
+        for (int u = 0; u < R - 1; ++u) add += base + (u + 1) * st - 1 < hi && a[u] <= b[u] ? st : 0;
+        base += add;
+    }
+    return base;
+}
+
+// radix 4: merge-split 0.251 -> 0.243 ms per whole-block stage of config 4 at
+// P = 8; radix 8 / 16 (more loads a round) 0.259 / 0.273
+// (profiles/r06/rankwork/corank_ab.txt)
+constexpr int CORANK_RADIX = 4;
 template <typename K>
 __global__ void k_merge_partition(const K* __restrict__ A, int64_t na, const K* __restrict__ B,
                                   int64_t nb, int64_t d0, int64_t nout, int64_t ntiles,
@@ -86,7 +118,7 @@ __global__ void k_merge_partition(const K* __restrict__ A, int64_t na, const K* 
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
     const int64_t off = t * MS_TILE < nout ? t * MS_TILE : nout;
-    co[t] = corank(A, na, B, nb, d0 + off);
+    co[t] = corank_r<CORANK_RADIX>(A, na, B, nb, d0 + off);
 }
 
 // Output keys [d0 + t*TILE, ...) of merge(A, B): each workgroup stages its A
