@@ -1082,9 +1082,12 @@ __global__ __launch_bounds__(DC_NT) void k_chunk_desc(const int64_t* __restrict_
 }
 
 // The chunks k_chunk_desc listed (ovf[1 .. ovf[0]]), each cut in two into
-// dov[2i], dov[2i + 1] (split_chunk): one wave per listed chunk, a small grid
-// (the list is usually empty: it exits at once; long only for adversarial runs).
-constexpr int SPLIT_WG = 64;
+// dov[2i], dov[2i + 1] (split_chunk): one wave per listed chunk (the list is
+// usually empty: every wave exits at once).  1024 waves, so that a long list --
+// inputs whose window offsets do not cancel -- is cut in parallel: with 64 a
+// 2^30 pass at a margin of 11 fences spent 260 us here
+// (profiles/r06/mergek/fm_add_ab.txt).
+constexpr int SPLIT_WG = 1024;
 template <typename KEY, int LK>
 __global__ __launch_bounds__(64) void k_split_desc(const KEY* __restrict__ src, const typename KTr<KEY>::F* __restrict__ F,
                                                   const typename KTr<KEY>::F* __restrict__ M, const int* __restrict__ P,
@@ -1271,11 +1274,13 @@ __device__ __forceinline__ void mergek_run(KEY* tile, const KEY* __restrict__ sr
     mergek_chunk<KEY, LK, FENCES, MODE, ORD>(s, d, dst, fout, lwn, lkn, tid);
 }
 
-// The grid: (capacity split) first OVF_WG workgroups that walk the halves of
+// The grid: (capacity split) first ovf_wg() workgroups that walk the halves of
 // the chunks k_split_desc cut (2 * ovf[0] descriptors in dov; usually none:
 // they exit at once; dispatched first, so a half never trails the pass), then
-// one workgroup per chunk.
-constexpr int OVF_WG = 256;
+// one workgroup per chunk.  One per resident slot of the chip (256 CUs x the
+// workgroups per CU), so the halves of a long list run in the first round.
+template <typename KEY, int LK>
+constexpr int ovf_wg() { return 256 * KTr<KEY>::wg(LK); }
 template <typename KEY, int LK, bool FENCES, int MODE = 0, bool ORD = false>
 __global__ __launch_bounds__(KTr<KEY>::NT, KTr<KEY>::wg(LK)* KTr<KEY>::NT / 256) void k_mergek(
     const KEY* __restrict__ src, KEY* __restrict__ dst, const Desc<KEY, LK>* __restrict__ desc,
@@ -1528,8 +1533,8 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
     if (split)
         k_split_desc<KEY, LK><<<SPLIT_WG, 64, 0, s>>>(src, F0, M0, P0, (const int*)bsum, cpb, geo,
                                                       (const int64_t*)bounds, ovf, dov, ew, line);
-    // the capacity split: OVF_WG more workgroups walk the cut chunks' halves
-    const unsigned grid = (unsigned)nchunks + (split ? OVF_WG : 0);
+    // the capacity split: ovf_wg more workgroups walk the cut chunks' halves
+    const unsigned grid = (unsigned)nchunks + (split ? ovf_wg<KEY, LK>() : 0);
     const uint32_t np = (uint32_t)nchunks;
     const Desc<KEY, LK>* dv = dov;
     const int* ov = ovf;
