@@ -1362,8 +1362,10 @@ int64_t chunks_of(const Geo& geo) {
 // 2^MISORT_FENCE_NEST_MIN fences (env; 0 = never): one HBM sweep of the fence
 // array instead of one per level.  Measured (profiles/r05/plan/nest_ab.txt):
 // 2^30 u32 passes 3 and 4 (2^23 fences) -30 us each, +0.6 %; at 2^22 fences
-// (2^29 keys) the nested pass's ~600 chunks underfill the chip: +5 us, so the
-// default threshold is 2^23.
+// (2^29 keys) the nested pass's ~600 chunks underfilled the chip: +5 us, so the
+// threshold was 2^23.  Round 6: with the nested pass's own planning in one
+// k_fence_rank launch, 2^21 measured 2^28 +0.5 %, 2^29 +0.6 %, 2^30 equal
+// (profiles/r06/plan/nest_ab.txt).
 constexpr int FENCE_NEST_LEVELS = 3;
 
 template <typename KEY, int LK>
@@ -1444,7 +1446,7 @@ hipError_t merge_pass(const KEY* src, KEY* dst, int64_t n, int lw, hipStream_t s
         bool nest = false;
         if constexpr (sizeof(KEY) == 4) {
             static const int nest_min =
-                getenv("MISORT_FENCE_NEST_MIN") ? atoi(getenv("MISORT_FENCE_NEST_MIN")) : 23;
+                getenv("MISORT_FENCE_NEST_MIN") ? atoi(getenv("MISORT_FENCE_NEST_MIN")) : 21;
             nest = depth == 0 && nest_min > 0 && left >= FENCE_NEST_LEVELS && nf >= ((int64_t)1 << nest_min) &&
                    wf_log2 + a >= KTr<uint64_t>::LW_MIN && wf_log2 + a + left <= KTr<uint64_t>::LWK_MAX;
         }
