@@ -222,7 +222,7 @@ ctx.close()
     (8, {"MISORT_FC_SLICES_MAX": "0", "MISORT_FENCE_RANK_MAX": "0"}, (1 << 22) + 3),
     (4, {"MISORT_RUN_FUSE": "2", "MISORT_MULTIWAY": "0"}, (1 << 22) + 4099),  # every 2-way level fused
     # fence merges as one nested u64 multi-way pass (the default from 2^21
-    # fences, i.e. 2^29 keys): 4 levels, 3 + 3 levels, 8-way passes
+    # fences, i.e. 2^28 keys): 4 levels, 3 + 3 levels, 8-way passes
     (4, {"MISORT_FENCE_NEST_MIN": "12"}, (1 << 26) + 12345),
     (4, {"MISORT_FENCE_NEST_MIN": "12"}, (1 << 27) + 777),
     (4, {"MISORT_FENCE_NEST_MIN": "12", "MISORT_MULTIWAY": "3"}, (1 << 26) + 12345),
